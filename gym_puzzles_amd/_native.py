@@ -1,0 +1,217 @@
+"""ctypes binding of ``libmrp.so`` (the HIP/gfx950 step library; C ABI in ``include/mrp.h``).
+
+The library is built in-tree by ``python -m gym_puzzles_amd.build`` (or
+``__graft_entry__.build()``).  There is no CPU fallback: if the shared object is missing
+or no HIP device is visible, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmrp.so")
+
+MRP_OK = 0
+STATUS_RUNNING, STATUS_PUZZLE_COMPLETE, STATUS_AGENT_OOB, STATUS_BLOCK_OOB = 0, 1, 2, 3
+
+ENV_IDS = {
+    "MultiRobotPuzzle-v0": 0,
+    "MultiRobotPuzzleHeavy-v0": 1,
+    "MultiRobotPuzzle-v2": 2,
+    "MultiRobotPuzzleHeavy-v2": 3,
+    "MultiRobotPuzzleHeavy-v2-3block": 4,
+}
+
+# every symbol include/mrp.h declares (tests/test_abi.py checks the .so exports all of them)
+EXPORTED = (
+    "mrp_env_dims", "mrp_create", "mrp_destroy", "mrp_last_error", "mrp_n_lanes", "mrp_env_id",
+    "mrp_set_stream", "mrp_synchronize", "mrp_set_reward_params", "mrp_update_params", "mrp_update_goal",
+    "mrp_reset", "mrp_reset_device", "mrp_step", "mrp_step_device", "mrp_set_auto_reset",
+    "mrp_get_bodies", "mrp_get_flags", "mrp_counters", "mrp_state_words", "mrp_get_state", "mrp_set_state",
+    "mrp_set_time_limit", "mrp_selftest_sincos",
+)
+
+_lib = None
+
+
+class MrpError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load libmrp.so (raises if it has not been built: there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MrpError(f"{LIB_PATH} not built; run `python -m gym_puzzles_amd.build` (hipcc, gfx950)")
+    L = ctypes.CDLL(LIB_PATH)
+    i, d, u64, P = ctypes.c_int, ctypes.c_double, ctypes.c_uint64, ctypes.c_void_p
+    ip = ctypes.POINTER(ctypes.c_int)
+    L.mrp_env_dims.argtypes = [i, ip, ip, ip, ip, ip, ip]
+    L.mrp_create.argtypes = [i, i, i, u64, u64, ctypes.POINTER(P)]
+    L.mrp_destroy.argtypes = [P]
+    L.mrp_destroy.restype = None
+    L.mrp_last_error.argtypes = [P]
+    L.mrp_last_error.restype = ctypes.c_char_p
+    L.mrp_n_lanes.argtypes = [P]
+    L.mrp_env_id.argtypes = [P]
+    L.mrp_set_stream.argtypes = [P, P]
+    L.mrp_synchronize.argtypes = [P]
+    L.mrp_set_reward_params.argtypes = [P, d, d, d, d, d, d, d]
+    L.mrp_update_params.argtypes = [P, d, d]
+    L.mrp_update_goal.argtypes = [P, d, d]
+    L.mrp_reset.argtypes = [P, P, P, P, P]
+    L.mrp_reset_device.argtypes = [P, P, P, P, P]
+    L.mrp_step.argtypes = [P, P, P, P, P, P, P, P]
+    L.mrp_step_device.argtypes = [P, P, P, P, P, P, P, P]
+    L.mrp_set_auto_reset.argtypes = [P, i]
+    L.mrp_get_bodies.argtypes = [P, P]
+    L.mrp_get_flags.argtypes = [P, P]
+    L.mrp_counters.argtypes = [P, P, P]
+    L.mrp_state_words.argtypes = [i]
+    L.mrp_get_state.argtypes = [P, P]
+    L.mrp_set_state.argtypes = [P, P]
+    L.mrp_set_time_limit.argtypes = [P, i]
+    L.mrp_selftest_sincos.argtypes = [i, P, P, P, i]
+    _lib = L
+    return L
+
+
+def env_dims(env_id: int) -> dict:
+    L = load()
+    vals = [ctypes.c_int() for _ in range(6)]
+    rc = L.mrp_env_dims(env_id, *[ctypes.byref(v) for v in vals])
+    if rc != MRP_OK:
+        raise ValueError(f"unknown env_id {env_id}")
+    keys = ("obs_dim", "act_dim", "n_draws", "n_agents", "n_blocks", "max_episode_steps")
+    return dict(zip(keys, (v.value for v in vals)))
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Batch:
+    """N independent MultiRobotPuzzle worlds on one GPU (one ``mrp_ctx``)."""
+
+    def __init__(self, env_id: int, n_lanes: int, device: int = 0, seed: int = 0, lane_offset: int = 0):
+        L = load()
+        self.env_id, self.n_lanes, self.device = env_id, n_lanes, device
+        self.__dict__.update(env_dims(env_id))
+        h = ctypes.c_void_p()
+        rc = L.mrp_create(env_id, n_lanes, device, seed, lane_offset, ctypes.byref(h))
+        if rc != MRP_OK:
+            raise MrpError(f"mrp_create failed ({rc}): {L.mrp_last_error(None).decode()}")
+        self._h = h
+        self.obs = np.zeros((n_lanes, self.obs_dim), np.float32)
+        self.reward = np.zeros(n_lanes, np.float32)
+        self.done = np.zeros(n_lanes, np.uint8)
+        self.truncated = np.zeros(n_lanes, np.uint8)
+        self.status = np.zeros(n_lanes, np.uint8)
+        self.terminal_obs = np.zeros((n_lanes, self.obs_dim), np.float32)
+
+    def _check(self, rc):
+        if rc != MRP_OK:
+            raise MrpError(load().mrp_last_error(self._h).decode())
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load().mrp_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_reward_params(self, agentDelta=None, agentDistance=None, blockDelta=None, blockDistance=None,
+                          puzzleComp=10000, outOfBounds=1000, blkOutOfBounds=100):
+        v0 = self.env_id < 2
+        agentDelta = 10 if agentDelta is None else agentDelta
+        agentDistance = (0.1 if v0 else 0.25) if agentDistance is None else agentDistance
+        blockDelta = (50 if v0 else 25) if blockDelta is None else blockDelta
+        blockDistance = (0.025 if v0 else 0.1) if blockDistance is None else blockDistance
+        self._check(load().mrp_set_reward_params(self._h, agentDelta, agentDistance, blockDelta, blockDistance,
+                                                 puzzleComp, outOfBounds, blkOutOfBounds))
+
+    def update_params(self, timestep, decay):
+        self._check(load().mrp_update_params(self._h, float(timestep), float(decay)))
+
+    def update_goal(self, epoch, nb_epochs):
+        self._check(load().mrp_update_goal(self._h, float(epoch), float(nb_epochs)))
+
+    def set_auto_reset(self, enabled: bool):
+        self._check(load().mrp_set_auto_reset(self._h, 1 if enabled else 0))
+
+    def reset(self, draws=None, actions=None, mask=None) -> np.ndarray:
+        d = None if draws is None else np.ascontiguousarray(draws, np.float64).reshape(self.n_lanes, self.n_draws)
+        a = None if actions is None else np.ascontiguousarray(actions, np.float32).reshape(self.n_lanes, self.act_dim)
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8).reshape(self.n_lanes)
+        self._check(load().mrp_reset(self._h, _p(m), _p(d), _p(a), _p(self.obs)))
+        return self.obs
+
+    def step(self, actions=None, want_terminal_obs=False):
+        a = None if actions is None else np.ascontiguousarray(actions, np.float32).reshape(self.n_lanes, self.act_dim)
+        term = self.terminal_obs if want_terminal_obs else None
+        self._check(load().mrp_step(self._h, _p(a), _p(self.obs), _p(self.reward), _p(self.done), _p(self.truncated),
+                                    _p(self.status), _p(term)))
+        return self.obs, self.reward, self.done, self.truncated
+
+    def step_device(self, d_actions, d_obs, d_reward=None, d_done=None, d_trunc=None, d_status=None, d_term=None):
+        """Asynchronous step on device pointers (ints, e.g. torch ``tensor.data_ptr()``)."""
+        self._check(load().mrp_step_device(self._h, d_actions, d_obs, d_reward, d_done, d_trunc, d_status, d_term))
+
+    def set_time_limit(self, max_episode_steps: int):
+        self._check(load().mrp_set_time_limit(self._h, int(max_episode_steps)))
+
+    def set_stream(self, stream_ptr):
+        self._check(load().mrp_set_stream(self._h, stream_ptr))
+
+    def synchronize(self):
+        self._check(load().mrp_synchronize(self._h))
+
+    def bodies(self) -> np.ndarray:
+        out = np.zeros((self.n_lanes, 6 * (self.n_agents + self.n_blocks)), np.float32)
+        self._check(load().mrp_get_bodies(self._h, _p(out)))
+        return out
+
+    def flags(self) -> np.ndarray:
+        out = np.zeros((self.n_lanes, self.n_agents + 1), np.int32)
+        self._check(load().mrp_get_flags(self._h, _p(out)))
+        return out
+
+    def counters(self):
+        a = np.zeros(1, np.int64)
+        b = np.zeros(1, np.int64)
+        self._check(load().mrp_counters(self._h, _p(a), _p(b)))
+        return int(a[0]), int(b[0])
+
+    def get_state(self) -> np.ndarray:
+        w = load().mrp_state_words(self.env_id)
+        out = np.zeros((self.n_lanes, w), np.uint32)
+        self._check(load().mrp_get_state(self._h, _p(out)))
+        return out
+
+    def set_state(self, state: np.ndarray):
+        s = np.ascontiguousarray(state, np.uint32)
+        self._check(load().mrp_set_state(self._h, _p(s)))
+
+
+def selftest_sincos(x: np.ndarray, device: int = 0):
+    """Evaluate the device sinf/cosf (glibc-faithful restatement) on ``x``."""
+    x = np.ascontiguousarray(x, np.float32)
+    s = np.zeros_like(x)
+    c = np.zeros_like(x)
+    rc = load().mrp_selftest_sincos(device, _p(x), _p(s), _p(c), x.size)
+    if rc != MRP_OK:
+        raise MrpError(f"mrp_selftest_sincos failed ({rc})")
+    return s, c

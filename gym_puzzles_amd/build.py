@@ -1,0 +1,49 @@
+"""Build libmrp.so in-tree with hipcc for gfx950 (``python -m gym_puzzles_amd.build``).
+
+Numerics flags are part of the contract: -ffp-contract=off (no FMA contraction, so float32
+expressions round exactly like the box2d-py engine), no fast-math, f32 denormals kept,
+correctly rounded f32 divide/sqrt.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "libmrp.so")
+SOURCES = [os.path.join(CSRC, "mrp_kernels.hip"), os.path.join(CSRC, "mrp_tables.cpp")]
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("mrp_math.h", "mrp_config.h", "mrp_world.h", "mrp_env.h", "mrp_tables.h")] + [
+    os.path.join(HERE, "..", "include", "mrp.h")]
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+         "-fno-gpu-flush-denormals-to-zero", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-strict-aliasing", "-fPIC", "-shared"]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.exists(c) or c == "hipcc"):
+            return c
+    return "hipcc"
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(OUT):
+        return False
+    t = os.path.getmtime(OUT)
+    return all(os.path.getmtime(d) <= t for d in DEPS if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and up_to_date():
+        return OUT
+    cmd = [hipcc()] + FLAGS + SOURCES + ["-o", OUT + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

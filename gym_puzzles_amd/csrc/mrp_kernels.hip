@@ -1,0 +1,515 @@
+// mrp_kernels.hip -- gfx950 kernels and the C ABI (include/mrp.h) of libmrp.so.
+//
+// Round-1 execution model: one GPU thread owns one world ("lane"); a 64-thread block is one
+// wave of 64 worlds.  The persistent lane state lives in HBM structure-of-arrays across lanes
+// (word w of lane l at state[w * n_lanes + l]) so each of the wave's state loads/stores is a
+// single coalesced 256-B transaction; the step itself runs on a private copy.  There is no
+// dense contraction anywhere in this path, so no MFMA: the work is scalar fp32 VALU with
+// data-dependent control flow (contacts, TOI), plus fp64 for the env-level arithmetic.
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/mrp.h"
+#include "mrp_env.h"
+#include "mrp_tables.h"
+
+using namespace mrp;
+
+__constant__ EnvTables g_tables[5];
+
+namespace {
+
+constexpr int BLOCK = 64;   // one wave per block: lanes of a block never wait on each other
+
+// LaneState is copied word-by-word; a may_alias word type keeps type-based alias analysis
+// from reordering these copies against the typed (float/int) accesses of the step code.
+typedef uint32_t __attribute__((__may_alias__)) word_t;
+
+template <int ENV>
+__device__ __forceinline__ void load_state(LaneState<ENV>& S, const uint32_t* __restrict__ g, int lane, int nl) {
+    word_t* w = reinterpret_cast<word_t*>(&S);
+    constexpr int NW = lane_words<ENV>();
+    for (int i = 0; i < NW; ++i) w[i] = g[(size_t)i * nl + lane];
+}
+template <int ENV>
+__device__ __forceinline__ void store_state(const LaneState<ENV>& S, uint32_t* __restrict__ g, int lane, int nl) {
+    const word_t* w = reinterpret_cast<const word_t*>(&S);
+    constexpr int NW = lane_words<ENV>();
+    for (int i = 0; i < NW; ++i) g[(size_t)i * nl + lane] = w[i];
+}
+
+template <int ENV>
+__global__ __launch_bounds__(BLOCK) void k_init(uint32_t* state, int nl) {
+    int lane = blockIdx.x * BLOCK + threadIdx.x;
+    if (lane >= nl) return;
+    LaneState<ENV> S;
+    memset(&S, 0, sizeof(S));
+    EnvParams P;
+    memset(&P, 0, sizeof(P));
+    Env<ENV> e(S, g_tables[ENV], P);
+    e.init_empty_world();
+    store_state<ENV>(S, state, lane, nl);
+}
+
+template <int ENV>
+__device__ void lane_reset(Env<ENV>& e, LaneState<ENV>& S, const double* draws, const float* actions, float* obs_row,
+                           int lane, uint64_t seed, uint64_t glane) {
+    using D = Dims<ENV>;
+    const EnvTables& T = g_tables[ENV];
+    double d[D::NDRAW];
+    float a[D::ACT];
+    uint64_t ctr = (uint64_t)(uint32_t)S.episode * 64u;
+    for (int k = 0; k < D::NDRAW; ++k)
+        d[k] = draws ? draws[(size_t)lane * D::NDRAW + k]
+                     : T.draw_lo[k] + (T.draw_hi[k] - T.draw_lo[k]) * rng_u01(seed, glane, 1, ctr + k);
+    for (int j = 0; j < D::ACT; ++j)
+        a[j] = actions ? actions[(size_t)lane * D::ACT + j] : (float)(-1.0 + 2.0 * rng_u01(seed, glane, 2, ctr + j));
+    S.episode += 1;
+    S.elapsed = 0;
+    float o[D::OBS];
+    e.env_reset(d, a, o);
+    for (int k = 0; k < D::OBS; ++k) obs_row[k] = o[k];
+}
+
+template <int ENV>
+__global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* state, int nl, const uint8_t* mask, const double* draws,
+                                                 const float* actions, float* obs, EnvParams P, uint64_t seed,
+                                                 uint64_t lane_offset) {
+    int lane = blockIdx.x * BLOCK + threadIdx.x;
+    if (lane >= nl) return;
+    if (mask && !mask[lane]) return;
+    LaneState<ENV> S;
+    load_state<ENV>(S, state, lane, nl);
+    Env<ENV> e(S, g_tables[ENV], P);
+    lane_reset<ENV>(e, S, draws, actions, obs + (size_t)lane * Dims<ENV>::OBS, lane, seed, lane_offset + lane);
+    store_state<ENV>(S, state, lane, nl);
+}
+
+template <int ENV>
+__global__ __launch_bounds__(BLOCK) void k_step(uint32_t* state, int nl, const float* actions, float* obs, float* reward,
+                                                uint8_t* done_out, uint8_t* trunc_out, uint8_t* status_out, float* term_obs,
+                                                EnvParams P, uint64_t seed, uint64_t lane_offset, int auto_reset,
+                                                int max_steps) {
+    using D = Dims<ENV>;
+    int lane = blockIdx.x * BLOCK + threadIdx.x;
+    if (lane >= nl) return;
+    LaneState<ENV> S;
+    load_state<ENV>(S, state, lane, nl);
+    Env<ENV> e(S, g_tables[ENV], P);
+    const uint64_t glane = lane_offset + lane;
+    float a[D::ACT];
+    uint64_t ctr = (uint64_t)S.stepCounter * 64u;
+    for (int j = 0; j < D::ACT; ++j)
+        a[j] = actions ? actions[(size_t)lane * D::ACT + j] : (float)(-1.0 + 2.0 * rng_u01(seed, glane, 3, ctr + j));
+    S.stepCounter += 1;
+    float o[D::OBS];
+    double r;
+    int d, kind;
+    e.env_step(a, o, r, d, kind);
+    S.elapsed += 1;
+    int tr = 0;
+    if (max_steps > 0 && S.elapsed >= max_steps) { tr = !d; d = 1; }   // gym TimeLimit
+    if (reward) reward[lane] = (float)r;
+    if (done_out) done_out[lane] = (uint8_t)d;
+    if (trunc_out) trunc_out[lane] = (uint8_t)tr;
+    if (status_out) status_out[lane] = (uint8_t)kind;
+    float* orow = obs + (size_t)lane * D::OBS;
+    if (term_obs) for (int k = 0; k < D::OBS; ++k) term_obs[(size_t)lane * D::OBS + k] = o[k];
+    if (d && auto_reset) lane_reset<ENV>(e, S, nullptr, nullptr, orow, lane, seed, glane);
+    else for (int k = 0; k < D::OBS; ++k) orow[k] = o[k];
+    store_state<ENV>(S, state, lane, nl);
+}
+
+__global__ __launch_bounds__(256) void k_sincos(const float* x, float* s, float* c, int n) {
+    int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    s[i] = g_sinf(x[i]);
+    c[i] = g_cosf(x[i]);
+}
+
+template <int ENV>
+__global__ __launch_bounds__(BLOCK) void k_bodies(const uint32_t* state, int nl, float* out, int32_t* flags) {
+    using D = Dims<ENV>;
+    int lane = blockIdx.x * BLOCK + threadIdx.x;
+    if (lane >= nl) return;
+    LaneState<ENV> S;
+    load_state<ENV>(S, state, lane, nl);
+    constexpr int ND = D::NA + D::NB;
+    if (out) {
+        float* r = out + (size_t)lane * 6 * ND;
+        for (int b = 0; b < ND; ++b) {
+            r[6 * b] = S.cx[b]; r[6 * b + 1] = S.cy[b]; r[6 * b + 2] = S.a[b];
+            r[6 * b + 3] = S.vx[b]; r[6 * b + 4] = S.vy[b]; r[6 * b + 5] = S.w[b];
+        }
+    }
+    if (flags) {
+        int32_t* f = flags + (size_t)lane * (D::NA + 1);
+        for (int i = 0; i < D::NA; ++i) f[i] = S.goal_contact[i];
+        f[D::NA] = S.blks_in_place;
+    }
+}
+
+// ------------------------------------------------------------------------------ host side
+thread_local std::string g_create_error;
+
+int grid_for(int nl) { return (nl + BLOCK - 1) / BLOCK; }
+
+}  // namespace
+
+struct mrp_ctx {
+    int env_id = 0, n_lanes = 0, device = 0;
+    uint64_t seed = 0, lane_offset = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;
+    uint32_t* d_state = nullptr;
+    EnvParams params{};
+    int auto_reset = 0;
+    int have_reset = 0;
+    int time_limit = 0;
+    double base_puzzle = 10000.0, base_bounds = 1000.0, base_blk_bounds = 100.0;   // set_reward_params
+    int shaped_set = 0;                                                             // update_params() called
+    int obs_dim = 0, act_dim = 0, n_draws = 0, n_agents = 0, n_blocks = 0, max_steps = 0, words = 0;
+    // staging buffers for the host-pointer API
+    double* d_draws = nullptr;
+    float* d_actions = nullptr;
+    uint8_t* d_mask = nullptr;
+    float* d_obs = nullptr;
+    float* d_reward = nullptr;
+    uint8_t* d_done = nullptr;
+    uint8_t* d_trunc = nullptr;
+    uint8_t* d_status = nullptr;
+    float* d_term = nullptr;
+    float* d_bodies = nullptr;
+    int32_t* d_flags = nullptr;
+    std::string err;
+};
+
+#define HIPCHK(ctx, expr)                                                   \
+    do {                                                                    \
+        hipError_t _e = (expr);                                             \
+        if (_e != hipSuccess) {                                             \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(_e); \
+            return MRP_E_HIP;                                               \
+        }                                                                   \
+    } while (0)
+
+#define DISPATCH(env, ...)                                \
+    switch (env) {                                        \
+    case 0: { constexpr int E = 0; __VA_ARGS__; } break; \
+    case 1: { constexpr int E = 1; __VA_ARGS__; } break; \
+    case 2: { constexpr int E = 2; __VA_ARGS__; } break; \
+    case 3: { constexpr int E = 3; __VA_ARGS__; } break; \
+    case 4: { constexpr int E = 4; __VA_ARGS__; } break; \
+    default: break;                                       \
+    }
+
+static int words_for(int env_id) {
+    int w = -1;
+    DISPATCH(env_id, w = lane_words<E>());
+    return w;
+}
+
+extern "C" {
+
+int mrp_env_dims(int env_id, int* obs_dim, int* act_dim, int* n_draws, int* n_agents, int* n_blocks, int* max_steps) {
+    EnvTables t;
+    if (!build_tables(env_id, t)) return MRP_E_ARG;
+    if (obs_dim) *obs_dim = t.obs_dim;
+    if (act_dim) *act_dim = t.act_dim;
+    if (n_draws) *n_draws = t.n_draws;
+    if (n_agents) *n_agents = t.n_agents;
+    if (n_blocks) *n_blocks = t.n_blocks;
+    if (max_steps) *max_steps = t.max_steps;
+    return MRP_OK;
+}
+
+int mrp_state_words(int env_id) { return words_for(env_id); }
+
+const char* mrp_last_error(const mrp_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
+int mrp_n_lanes(const mrp_ctx* ctx) { return ctx ? ctx->n_lanes : MRP_E_ARG; }
+int mrp_env_id(const mrp_ctx* ctx) { return ctx ? ctx->env_id : MRP_E_ARG; }
+
+void mrp_destroy(mrp_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    void* bufs[] = {ctx->d_state, ctx->d_draws, ctx->d_actions, ctx->d_mask, ctx->d_obs, ctx->d_reward, ctx->d_done,
+                    ctx->d_trunc, ctx->d_status, ctx->d_term, ctx->d_bodies, ctx->d_flags};
+    for (void* p : bufs)
+        if (p) (void)hipFree(p);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+}
+
+int mrp_create(int env_id, int n_lanes, int device, uint64_t seed, uint64_t lane_offset, mrp_ctx** out) {
+    g_create_error.clear();
+    if (!out) { g_create_error = "out is NULL"; return MRP_E_ARG; }
+    *out = nullptr;
+    EnvTables tables;
+    if (!build_tables(env_id, tables)) { g_create_error = "bad env_id"; return MRP_E_ARG; }
+    if (n_lanes <= 0) { g_create_error = "n_lanes must be > 0"; return MRP_E_ARG; }
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0) {
+        g_create_error = "no HIP device available (libmrp has no CPU fallback)";
+        return MRP_E_HIP;
+    }
+    if (device < 0 || device >= ndev) { g_create_error = "device index out of range"; return MRP_E_ARG; }
+    mrp_ctx* ctx = new (std::nothrow) mrp_ctx();
+    if (!ctx) { g_create_error = "out of host memory"; return MRP_E_ARG; }
+    ctx->env_id = env_id; ctx->n_lanes = n_lanes; ctx->device = device; ctx->seed = seed; ctx->lane_offset = lane_offset;
+    ctx->obs_dim = tables.obs_dim; ctx->act_dim = tables.act_dim; ctx->n_draws = tables.n_draws;
+    ctx->n_agents = tables.n_agents; ctx->n_blocks = tables.n_blocks; ctx->max_steps = tables.max_steps;
+    ctx->words = words_for(env_id);
+    ctx->time_limit = tables.max_steps;
+    default_params(env_id, ctx->params);
+    auto fail = [&](const char* what, hipError_t he) {
+        g_create_error = std::string(what) + ": " + hipGetErrorString(he);
+        mrp_destroy(ctx);
+        return MRP_E_HIP;
+    };
+    if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
+    EnvTables all[5];
+    for (int i = 0; i < 5; ++i) build_tables(i, all[i]);
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_tables), all, sizeof(all))) != hipSuccess) return fail("hipMemcpyToSymbol", e);
+    if ((e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking)) != hipSuccess) return fail("hipStreamCreate", e);
+    ctx->stream = ctx->own_stream;
+    size_t nl = (size_t)n_lanes;
+    struct { void** p; size_t bytes; } allocs[] = {
+        {(void**)&ctx->d_state, (size_t)ctx->words * nl * 4},
+        {(void**)&ctx->d_draws, nl * ctx->n_draws * sizeof(double)},
+        {(void**)&ctx->d_actions, nl * ctx->act_dim * sizeof(float)},
+        {(void**)&ctx->d_mask, nl},
+        {(void**)&ctx->d_obs, nl * ctx->obs_dim * sizeof(float)},
+        {(void**)&ctx->d_term, nl * ctx->obs_dim * sizeof(float)},
+        {(void**)&ctx->d_reward, nl * sizeof(float)},
+        {(void**)&ctx->d_done, nl},
+        {(void**)&ctx->d_trunc, nl},
+        {(void**)&ctx->d_status, nl},
+        {(void**)&ctx->d_bodies, nl * 6 * (ctx->n_agents + ctx->n_blocks) * sizeof(float)},
+        {(void**)&ctx->d_flags, nl * (ctx->n_agents + 1) * sizeof(int32_t)},
+    };
+    for (auto& a : allocs)
+        if ((e = hipMalloc(a.p, a.bytes)) != hipSuccess) return fail("hipMalloc", e);
+    DISPATCH(env_id, hipLaunchKernelGGL(k_init<E>, dim3(grid_for(n_lanes)), dim3(BLOCK), 0, ctx->stream, ctx->d_state, n_lanes));
+    if ((e = hipGetLastError()) != hipSuccess) return fail("k_init launch", e);
+    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return fail("k_init", e);
+    *out = ctx;
+    return MRP_OK;
+}
+
+int mrp_set_stream(mrp_ctx* ctx, void* hip_stream) {
+    if (!ctx) return MRP_E_ARG;
+    ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+    return MRP_OK;
+}
+
+int mrp_synchronize(mrp_ctx* ctx) {
+    if (!ctx) return MRP_E_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return MRP_OK;
+}
+
+int mrp_set_reward_params(mrp_ctx* ctx, double agent_delta, double agent_distance, double block_delta, double block_distance,
+                          double puzzle_comp, double out_of_bounds, double blk_out_of_bounds) {
+    if (!ctx) return MRP_E_ARG;
+    ctx->params.w_dAgent = agent_delta; ctx->params.w_agentDist = agent_distance;
+    ctx->params.w_dBlock = block_delta; ctx->params.w_blkDist = block_distance;
+    ctx->base_puzzle = puzzle_comp; ctx->base_bounds = out_of_bounds; ctx->base_blk_bounds = blk_out_of_bounds;
+    // shaped_* are derived only by update_params() (the reference leaves them undefined until
+    // then); the batched default before that call is decay = 1, timestep = 0
+    if (!ctx->shaped_set) {
+        ctx->params.shaped_puzzle = puzzle_comp; ctx->params.shaped_bounds = out_of_bounds;
+        ctx->params.shaped_blk_bounds = blk_out_of_bounds;
+    }
+    return MRP_OK;
+}
+
+int mrp_update_params(mrp_ctx* ctx, double timestep, double decay) {
+    if (!ctx) return MRP_E_ARG;
+    double f = pow(decay, -timestep);   // _02.py:227-230: penalty * decay ** (-timestep)
+    ctx->params.shaped_bounds = ctx->base_bounds * f;
+    ctx->params.shaped_blk_bounds = ctx->base_blk_bounds * f;
+    ctx->params.shaped_puzzle = ctx->base_puzzle * f;
+    ctx->shaped_set = 1;
+    return MRP_OK;
+}
+
+int mrp_update_goal(mrp_ctx* ctx, double epoch, double nb_epochs) {
+    if (!ctx) return MRP_E_ARG;
+    double eps = ctx->env_id < 2 ? 25.0 : 0.1;
+    ctx->params.scaled_epsilon = eps * (2 - epoch / nb_epochs);
+    return MRP_OK;
+}
+
+int mrp_set_auto_reset(mrp_ctx* ctx, int enabled) {
+    if (!ctx) return MRP_E_ARG;
+    ctx->auto_reset = enabled ? 1 : 0;
+    return MRP_OK;
+}
+
+int mrp_set_time_limit(mrp_ctx* ctx, int max_episode_steps) {
+    if (!ctx || max_episode_steps < 0) return MRP_E_ARG;
+    ctx->time_limit = max_episode_steps;
+    return MRP_OK;
+}
+
+int mrp_reset_device(mrp_ctx* ctx, const uint8_t* d_mask, const double* d_draws, const float* d_actions, float* d_obs) {
+    if (!ctx || !d_obs) return MRP_E_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    DISPATCH(ctx->env_id, hipLaunchKernelGGL(k_reset<E>, dim3(grid_for(ctx->n_lanes)), dim3(BLOCK), 0, ctx->stream, ctx->d_state,
+                                             ctx->n_lanes, d_mask, d_draws, d_actions, d_obs, ctx->params, ctx->seed,
+                                             ctx->lane_offset));
+    HIPCHK(ctx, hipGetLastError());
+    ctx->have_reset = 1;
+    return MRP_OK;
+}
+
+int mrp_reset(mrp_ctx* ctx, const uint8_t* mask, const double* draws, const float* actions, float* obs) {
+    if (!ctx || !obs) return MRP_E_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    size_t nl = (size_t)ctx->n_lanes;
+    if (mask) HIPCHK(ctx, hipMemcpyAsync(ctx->d_mask, mask, nl, hipMemcpyHostToDevice, ctx->stream));
+    if (draws)
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_draws, draws, nl * ctx->n_draws * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    if (actions)
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_actions, actions, nl * ctx->act_dim * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    // rows of unmasked lanes stay as the caller had them
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_obs, obs, nl * ctx->obs_dim * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    int rc = mrp_reset_device(ctx, mask ? ctx->d_mask : nullptr, draws ? ctx->d_draws : nullptr,
+                              actions ? ctx->d_actions : nullptr, ctx->d_obs);
+    if (rc) return rc;
+    HIPCHK(ctx, hipMemcpyAsync(obs, ctx->d_obs, nl * ctx->obs_dim * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return MRP_OK;
+}
+
+int mrp_step_device(mrp_ctx* ctx, const float* d_actions, float* d_obs, float* d_reward, uint8_t* d_done, uint8_t* d_trunc,
+                    uint8_t* d_status, float* d_term) {
+    if (!ctx || !d_obs) return MRP_E_ARG;
+    if (!ctx->have_reset) { ctx->err = "step() called before reset()"; return MRP_E_STATE; }
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    DISPATCH(ctx->env_id, hipLaunchKernelGGL(k_step<E>, dim3(grid_for(ctx->n_lanes)), dim3(BLOCK), 0, ctx->stream, ctx->d_state,
+                                             ctx->n_lanes, d_actions, d_obs, d_reward, d_done, d_trunc, d_status, d_term,
+                                             ctx->params, ctx->seed, ctx->lane_offset, ctx->auto_reset, ctx->time_limit));
+    HIPCHK(ctx, hipGetLastError());
+    return MRP_OK;
+}
+
+int mrp_step(mrp_ctx* ctx, const float* actions, float* obs, float* reward, uint8_t* done, uint8_t* trunc, uint8_t* status,
+             float* term) {
+    if (!ctx || !obs) return MRP_E_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    size_t nl = (size_t)ctx->n_lanes;
+    if (actions)
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_actions, actions, nl * ctx->act_dim * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    int rc = mrp_step_device(ctx, actions ? ctx->d_actions : nullptr, ctx->d_obs, ctx->d_reward, ctx->d_done, ctx->d_trunc,
+                             ctx->d_status, term ? ctx->d_term : nullptr);
+    if (rc) return rc;
+    HIPCHK(ctx, hipMemcpyAsync(obs, ctx->d_obs, nl * ctx->obs_dim * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    if (reward) HIPCHK(ctx, hipMemcpyAsync(reward, ctx->d_reward, nl * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    if (done) HIPCHK(ctx, hipMemcpyAsync(done, ctx->d_done, nl, hipMemcpyDeviceToHost, ctx->stream));
+    if (trunc) HIPCHK(ctx, hipMemcpyAsync(trunc, ctx->d_trunc, nl, hipMemcpyDeviceToHost, ctx->stream));
+    if (status) HIPCHK(ctx, hipMemcpyAsync(status, ctx->d_status, nl, hipMemcpyDeviceToHost, ctx->stream));
+    if (term)
+        HIPCHK(ctx, hipMemcpyAsync(term, ctx->d_term, nl * ctx->obs_dim * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return MRP_OK;
+}
+
+int mrp_get_bodies(mrp_ctx* ctx, float* out) {
+    if (!ctx || !out) return MRP_E_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    DISPATCH(ctx->env_id, hipLaunchKernelGGL(k_bodies<E>, dim3(grid_for(ctx->n_lanes)), dim3(BLOCK), 0, ctx->stream, ctx->d_state,
+                                             ctx->n_lanes, ctx->d_bodies, (int32_t*)nullptr));
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemcpyAsync(out, ctx->d_bodies, (size_t)ctx->n_lanes * 6 * (ctx->n_agents + ctx->n_blocks) * sizeof(float),
+                               hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return MRP_OK;
+}
+
+int mrp_get_flags(mrp_ctx* ctx, int32_t* out) {
+    if (!ctx || !out) return MRP_E_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    DISPATCH(ctx->env_id, hipLaunchKernelGGL(k_bodies<E>, dim3(grid_for(ctx->n_lanes)), dim3(BLOCK), 0, ctx->stream, ctx->d_state,
+                                             ctx->n_lanes, (float*)nullptr, ctx->d_flags));
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemcpyAsync(out, ctx->d_flags, (size_t)ctx->n_lanes * (ctx->n_agents + 1) * sizeof(int32_t),
+                               hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return MRP_OK;
+}
+
+int mrp_get_state(mrp_ctx* ctx, uint32_t* out) {
+    if (!ctx || !out) return MRP_E_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    size_t nl = (size_t)ctx->n_lanes, nw = (size_t)ctx->words;
+    std::vector<uint32_t> soa(nl * nw);
+    HIPCHK(ctx, hipMemcpyAsync(soa.data(), ctx->d_state, nl * nw * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    for (size_t w = 0; w < nw; ++w)
+        for (size_t l = 0; l < nl; ++l) out[l * nw + w] = soa[w * nl + l];
+    return MRP_OK;
+}
+
+int mrp_set_state(mrp_ctx* ctx, const uint32_t* in) {
+    if (!ctx || !in) return MRP_E_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    size_t nl = (size_t)ctx->n_lanes, nw = (size_t)ctx->words;
+    std::vector<uint32_t> soa(nl * nw);
+    for (size_t w = 0; w < nw; ++w)
+        for (size_t l = 0; l < nl; ++l) soa[w * nl + l] = in[l * nw + w];
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_state, soa.data(), nl * nw * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->have_reset = 1;
+    return MRP_OK;
+}
+
+int mrp_counters(mrp_ctx* ctx, int64_t* toi_events, int64_t* pos_iters) {
+    if (!ctx) return MRP_E_ARG;
+    size_t nl = (size_t)ctx->n_lanes, nw = (size_t)ctx->words;
+    std::vector<uint32_t> st(nl * nw);
+    int rc = mrp_get_state(ctx, st.data());
+    if (rc) return rc;
+    size_t off = 0;
+    DISPATCH(ctx->env_id, off = offsetof(LaneState<E>, toiEvents) / 4);
+    int64_t toi = 0, pos = 0;
+    for (size_t l = 0; l < nl; ++l) {
+        int64_t a, b;
+        std::memcpy(&a, &st[l * nw + off], 8);
+        std::memcpy(&b, &st[l * nw + off + 2], 8);
+        toi += a; pos += b;
+    }
+    if (toi_events) *toi_events = toi;
+    if (pos_iters) *pos_iters = pos;
+    return MRP_OK;
+}
+
+int mrp_selftest_sincos(int device, const float* x, float* sin_out, float* cos_out, int n) {
+    if (!x || !sin_out || !cos_out || n <= 0) return MRP_E_ARG;
+    if (hipSetDevice(device) != hipSuccess) return MRP_E_HIP;
+    float *dx = nullptr, *ds = nullptr, *dc = nullptr;
+    size_t bytes = (size_t)n * sizeof(float);
+    int rc = MRP_E_HIP;
+    if (hipMalloc(&dx, bytes) == hipSuccess && hipMalloc(&ds, bytes) == hipSuccess && hipMalloc(&dc, bytes) == hipSuccess &&
+        hipMemcpy(dx, x, bytes, hipMemcpyHostToDevice) == hipSuccess) {
+        hipLaunchKernelGGL(k_sincos, dim3((n + 255) / 256), dim3(256), 0, 0, dx, ds, dc, n);
+        if (hipGetLastError() == hipSuccess && hipMemcpy(sin_out, ds, bytes, hipMemcpyDeviceToHost) == hipSuccess &&
+            hipMemcpy(cos_out, dc, bytes, hipMemcpyDeviceToHost) == hipSuccess)
+            rc = MRP_OK;
+    }
+    if (dx) (void)hipFree(dx);
+    if (ds) (void)hipFree(ds);
+    if (dc) (void)hipFree(dc);
+    return rc;
+}
+
+}  // extern "C"

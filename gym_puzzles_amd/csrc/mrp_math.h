@@ -1,0 +1,184 @@
+// mrp_math.h -- float32 vector math with Box2D v2.3 operation order, glibc-faithful
+// sinf/cosf, and the counter RNG.  Compiled for gfx950 device code and for the host
+// (geometry tables); both sides MUST be built with -ffp-contract=off and without
+// fast-math so every expression rounds exactly like the box2d-py engine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MRP_HD __host__ __device__ __forceinline__
+
+namespace mrp {
+
+struct V2 { float x, y; };
+struct Rot { float s, c; };
+struct Xf { V2 p; Rot q; };
+
+MRP_HD V2 v2(float x, float y) { V2 r; r.x = x; r.y = y; return r; }
+MRP_HD V2 vadd(V2 a, V2 b) { return v2(a.x + b.x, a.y + b.y); }
+MRP_HD V2 vsub(V2 a, V2 b) { return v2(a.x - b.x, a.y - b.y); }
+MRP_HD V2 vmul(float s, V2 a) { return v2(s * a.x, s * a.y); }   // b2Vec2 operator*(float, b2Vec2)
+MRP_HD V2 vneg(V2 a) { return v2(-a.x, -a.y); }
+MRP_HD float vdot(V2 a, V2 b) { return a.x * b.x + a.y * b.y; }
+MRP_HD float vcross(V2 a, V2 b) { return a.x * b.y - a.y * b.x; }
+MRP_HD V2 vcross_vs(V2 a, float s) { return v2(s * a.y, -s * a.x); }
+MRP_HD V2 vcross_sv(float s, V2 a) { return v2(-s * a.y, s * a.x); }
+MRP_HD float vlensq(V2 a) { return a.x * a.x + a.y * a.y; }
+MRP_HD float vlen(V2 a) { return sqrtf(a.x * a.x + a.y * a.y); }
+MRP_HD float vnormalize(V2& a) {
+    float length = sqrtf(a.x * a.x + a.y * a.y);
+    if (length < 1.1920928955078125e-7f) return 0.0f;   // b2_epsilon = FLT_EPSILON
+    float inv = 1.0f / length;
+    a.x *= inv; a.y *= inv;
+    return length;
+}
+MRP_HD float fmin_(float a, float b) { return a < b ? a : b; }
+MRP_HD float fmax_(float a, float b) { return a > b ? a : b; }
+MRP_HD float fclamp(float a, float lo, float hi) { return fmax_(lo, fmin_(a, hi)); }
+MRP_HD V2 vmin(V2 a, V2 b) { return v2(fmin_(a.x, b.x), fmin_(a.y, b.y)); }
+MRP_HD V2 vmax(V2 a, V2 b) { return v2(fmax_(a.x, b.x), fmax_(a.y, b.y)); }
+MRP_HD V2 mul_rv(Rot q, V2 v) { return v2(q.c * v.x - q.s * v.y, q.s * v.x + q.c * v.y); }
+MRP_HD V2 mulT_rv(Rot q, V2 v) { return v2(q.c * v.x + q.s * v.y, -q.s * v.x + q.c * v.y); }
+MRP_HD V2 mul_xv(Xf T, V2 v) {
+    float x = (T.q.c * v.x - T.q.s * v.y) + T.p.x;
+    float y = (T.q.s * v.x + T.q.c * v.y) + T.p.y;
+    return v2(x, y);
+}
+MRP_HD V2 mulT_xv(Xf T, V2 v) {
+    float px = v.x - T.p.x, py = v.y - T.p.y;
+    return v2(T.q.c * px + T.q.s * py, -T.q.s * px + T.q.c * py);
+}
+MRP_HD Rot mulT_rr(Rot q, Rot r) { Rot o; o.s = q.c * r.s - q.s * r.c; o.c = q.c * r.c + q.s * r.s; return o; }
+MRP_HD Xf mulT_xx(Xf A, Xf B) { Xf C; C.q = mulT_rr(A.q, B.q); C.p = mulT_rv(A.q, vsub(B.p, A.p)); return C; }
+
+// ---------------------------------------------------------------------------------------
+// sinf / cosf, bit-exact with glibc >= 2.28's FMA code path (sysdeps/ieee754/flt-32
+// s_sinf.c / s_cosf.c, the variant glibc's ifunc selects on every FMA-capable x86-64 CPU).
+// Verified exhaustively against the host glibc 2.35 sinf/cosf over all 4,278,190,080
+// finite float inputs (tests/test_sincos.py re-checks a strided subset).  Box2D calls
+// sinf/cosf in every b2Rot::Set, so sharing one exact implementation is what makes the
+// GPU trajectory bitwise equal to the CPU one.
+// ---------------------------------------------------------------------------------------
+struct SinCosT { double sign[4]; double hpi_inv, hpi, c0, c1, c2, c3, c4, s1, s2, s3; };
+
+MRP_HD const SinCosT& sincos_table(int k) {
+    // 2/pi * 2^24, pi/2, then the cos (c0..c4) and sin (s1..s3) minimax coefficients.
+    static constexpr SinCosT T0 = {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0,
+        0x1p0, -0x1.ffffffd0c621cp-2, 0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10, 0x1.99343027bf8c3p-16,
+        -0x1.555545995a603p-3, 0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13};
+    static constexpr SinCosT T1 = {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0,
+        -0x1p0, 0x1.ffffffd0c621cp-2, -0x1.55553e1068f19p-5, 0x1.6c087e89a359dp-10, -0x1.99343027bf8c3p-16,
+        -0x1.555545995a603p-3, 0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13};
+    return k ? T1 : T0;
+}
+
+MRP_HD uint32_t f2u(float f) { union { float f; uint32_t u; } x; x.f = f; return x.u; }
+MRP_HD float u2f(uint32_t u) { union { float f; uint32_t u; } x; x.u = u; return x.f; }
+MRP_HD uint32_t abstop12(float x) { return (f2u(x) >> 20) & 0x7ff; }
+
+MRP_HD float sincos_poly(double x, double x2, const SinCosT& p, int n) {
+    if ((n & 1) == 0) {
+        double x3 = x * x2;
+        double s1 = fma(x2, p.s3, p.s2);
+        double x7 = x3 * x2;
+        double s = fma(x3, p.s1, x);
+        return (float)fma(x7, s1, s);
+    } else {
+        double x4 = x2 * x2;
+        double c2 = fma(x2, p.c4, p.c3);
+        double c1 = fma(x2, p.c1, p.c0);
+        double x6 = x4 * x2;
+        double c = fma(x4, p.c2, c1);
+        return (float)fma(x6, c2, c);
+    }
+}
+
+MRP_HD double reduce_fast(double x, const SinCosT& p, int* np) {
+    double r = x * p.hpi_inv;
+    int n = ((int32_t)r + 0x800000) >> 24;
+    *np = n;
+    return fma(-(double)n, p.hpi, x);
+}
+
+MRP_HD double reduce_large(uint32_t xi, int* np) {
+    // bits of 2/pi (glibc __inv_pio4)
+    const uint32_t inv_pio4[24] = {0xa2, 0xa2f9, 0xa2f983, 0xa2f9836e, 0xf9836e4e, 0x836e4e44, 0x6e4e4415, 0x4e441529,
+        0x441529fc, 0x1529fc27, 0x29fc2757, 0xfc2757d1, 0x2757d1f5, 0x57d1f534, 0xd1f534dd, 0xf534ddc0,
+        0x34ddc0db, 0xddc0db62, 0xc0db6295, 0xdb629599, 0x6295993c, 0x95993c43, 0x993c4390, 0x3c439041};
+    const uint32_t* arr = &inv_pio4[(xi >> 26) & 15];
+    int shift = (xi >> 23) & 7;
+    uint64_t n, res0, res1, res2;
+    xi = (xi & 0xffffff) | 0x800000;
+    xi <<= shift;
+    res0 = xi * arr[0];
+    res1 = (uint64_t)xi * arr[4];
+    res2 = (uint64_t)xi * arr[8];
+    res0 = (res2 >> 32) | (res0 << 32);
+    res0 += res1;
+    n = (res0 + (1ULL << 61)) >> 62;
+    res0 -= n << 62;
+    double x = (double)(int64_t)res0;
+    *np = (int)n;
+    return x * 0x1.921FB54442D18p-62;
+}
+
+MRP_HD float g_sinf(float y) {
+    double x = y, s; int n;
+    if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {
+        s = x * x;
+        if (abstop12(y) < abstop12(0x1p-12f)) return y;
+        return sincos_poly(x, s, sincos_table(0), 0);
+    } else if (abstop12(y) < abstop12(120.0f)) {
+        x = reduce_fast(x, sincos_table(0), &n);
+        s = sincos_table(0).sign[n & 3];
+        const SinCosT& p = sincos_table((n & 2) ? 1 : 0);
+        return sincos_poly(x * s, x * x, p, n);
+    } else if (abstop12(y) < abstop12(__builtin_inff())) {
+        uint32_t xi = f2u(y); int sign = xi >> 31;
+        x = reduce_large(xi, &n);
+        s = sincos_table(0).sign[(n + sign) & 3];
+        const SinCosT& p = sincos_table(((n + sign) & 2) ? 1 : 0);
+        return sincos_poly(x * s, x * x, p, n);
+    }
+    return (y - y) / (y - y);
+}
+
+MRP_HD float g_cosf(float y) {
+    double x = y, s; int n;
+    if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {
+        double x2 = x * x;
+        if (abstop12(y) < abstop12(0x1p-12f)) return 1.0f;
+        return sincos_poly(x, x2, sincos_table(0), 1);
+    } else if (abstop12(y) < abstop12(120.0f)) {
+        x = reduce_fast(x, sincos_table(0), &n);
+        s = sincos_table(0).sign[n & 3];
+        const SinCosT& p = sincos_table((n & 2) ? 1 : 0);
+        return sincos_poly(x * s, x * x, p, n ^ 1);
+    } else if (abstop12(y) < abstop12(__builtin_inff())) {
+        uint32_t xi = f2u(y); int sign = xi >> 31;
+        x = reduce_large(xi, &n);
+        s = sincos_table(0).sign[(n + sign) & 3];
+        const SinCosT& p = sincos_table(((n + sign) & 2) ? 1 : 0);
+        return sincos_poly(x * s, x * x, p, n ^ 1);
+    }
+    return (y - y) / (y - y);
+}
+
+MRP_HD Rot rot(float angle) { Rot q; q.s = g_sinf(angle); q.c = g_cosf(angle); return q; }
+
+// ---------------------------------------------------------------------------------------
+// Counter-based RNG for on-device resets and synthetic actions (pure integer SplitMix64
+// mixing; identical on host and device, so the CPU oracle can replay device resets).
+// ---------------------------------------------------------------------------------------
+MRP_HD uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+MRP_HD double rng_u01(uint64_t seed, uint64_t lane, uint64_t stream, uint64_t counter) {
+    uint64_t h = splitmix64(seed ^ splitmix64(lane ^ splitmix64(stream ^ splitmix64(counter))));
+    return (double)(h >> 11) * 0x1.0p-53;
+}
+
+}  // namespace mrp

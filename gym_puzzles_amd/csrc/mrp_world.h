@@ -1,0 +1,1233 @@
+// mrp_world.h -- one MultiRobotPuzzle world ("lane") stepped by one GPU thread.
+//
+// This is the MI355X-native restatement of the per-timestep path of
+// gym_puzzles/envs/multi_robot_puzzle_00.py:413-521 (v0) and multi_robot_puzzle_02.py:444-584
+// (v2): action -> forces, the Box2D v2.3 world.Step(1/50, 180, 60) (broad phase, polygon SAT,
+// sequential-impulse contact solver with the 2-point block solver, position solver, TOI),
+// then contact flags, distances, observation, reward, done.
+//
+// Layout: the persistent lane state (LaneState<ENV>) is a POD of 32-bit words stored
+// structure-of-arrays across lanes in HBM (word w of lane l at base[w * n_lanes + l]), so
+// the wave's 64 lanes read/write each word coalesced.  Inside a step the thread works on a
+// private copy; per-step temporaries (islands, constraints) are private arrays.
+//
+// Box2D's pointer-linked lists become index lists: the world contact list is a doubly
+// linked list of slots in creation-descending order, and a body's contact-edge list is the
+// world list filtered by that body (same relative order, since both are head-inserted at
+// contact creation).  The dynamic AABB tree is kept node-for-node (same allocation order,
+// SAH insertion, rotations) because its free list decides the proxy ids after a reset, and
+// proxy ids decide fixture A/B roles and the contact (= Gauss-Seidel) order.
+#pragma once
+#include "mrp_config.h"
+
+namespace mrp {
+
+constexpr int NULLN = -1;
+constexpr float LINEAR_SLOP = 0.005f;
+constexpr float AABB_EXT = 0.1f;
+constexpr float AABB_MUL = 2.0f;
+constexpr float MAX_TRANSLATION = 2.0f;
+constexpr float MAX_TRANSLATION_SQ = MAX_TRANSLATION * MAX_TRANSLATION;
+constexpr float B2_PI = 3.14159265359f;
+constexpr float MAX_ROTATION = 0.5f * B2_PI;
+constexpr float MAX_ROTATION_SQ = MAX_ROTATION * MAX_ROTATION;
+constexpr float BAUMGARTE = 0.2f;
+constexpr float TOI_BAUMGARTE = 0.75f;
+constexpr float VELOCITY_THRESHOLD = 1.0f;
+constexpr float MAX_LINEAR_CORRECTION = 0.2f;
+constexpr int MAX_SUBSTEPS = 8;
+constexpr int MAX_TOI_CONTACTS = 32;
+constexpr float FLT_EPS = 1.1920928955078125e-7f;
+constexpr float FLT_MAXV = 3.40282346638528859811704183484516925e+38f;
+
+// contact flags (b2Contact)
+constexpr int CF_ISLAND = 1, CF_TOUCHING = 2, CF_ENABLED = 4, CF_TOI = 32;
+constexpr int MT_FACEA = 1, MT_FACEB = 2;
+
+template <int ENV> struct LaneState {
+    using D = Dims<ENV>;
+    static constexpr int ND = D::NA + D::NB;
+    static constexpr int C = D::CMAX;
+    // dynamic bodies (blocks, then agents): transform, sweep, velocity, force accumulators
+    float xpx[ND], xpy[ND], xs[ND], xc[ND];
+    float c0x[ND], c0y[ND], cx[ND], cy[ND], a0[ND], a[ND], alpha0[ND];
+    float vx[ND], vy[ND], w[ND];
+    float fx[ND], fy[ND], tq[ND];
+    // fixtures -> broad-phase proxy id
+    int proxy[D::NF];
+    // dynamic AABB tree (fat AABBs)
+    float tlx[TREE_N], tly[TREE_N], thx[TREE_N], thy[TREE_N];
+    int tpar[TREE_N], tc1[TREE_N], tc2[TREE_N], th[TREE_N], tud[TREE_N];
+    int root, freeList, nodeCount, moveCount;
+    int moveBuf[MOVE_N];
+    // contacts (slot pool + creation-descending doubly linked list)
+    int cHead, cFree, cCount, pad0;
+    int cnext[C], cprev[C], cfa[C], cfb[C], cflags[C], ctoiCount[C];
+    float ctoi[C], cfric[C];
+    int mpc[C], mtype[C];
+    float mlnx[C], mlny[C], mlpx[C], mlpy[C];
+    float mpx[2][C], mpy[2][C], mni[2][C], mti[2][C];
+    uint32_t mid[2][C];
+    // world
+    float inv_dt0;
+    int newFixture, haveBodies, episode;
+    uint32_t stepCounter;
+    int elapsed, blks_in_place, prev_blks_in_place;
+    int goal_contact[D::NA];
+    int wall_contact, pad1;
+    double agent_dist[D::NA];
+    double block_distance[D::NB];
+    double goal[D::NB][3];
+    long long toiEvents, posIters;
+};
+
+template <int ENV> constexpr int lane_words() { return (int)(sizeof(LaneState<ENV>) / 4); }
+
+struct TOIOut { int state; float t; };
+
+template <int ENV> struct World {
+    using D = Dims<ENV>;
+    using LS = LaneState<ENV>;
+    static constexpr int NA = D::NA, NB = D::NB, ND = LS::ND, NBODY = ND + 4, NF = D::NF, C = D::CMAX;
+
+    LS& S;
+    const EnvTables& T;
+    const EnvParams& P;
+
+    __device__ World(LS& s, const EnvTables& t, const EnvParams& p) : S(s), T(t), P(p) {}
+
+    // ------------------------------------------------------------------ bodies
+    __device__ bool is_dyn(int b) const { return b < ND; }
+    __device__ Xf xf(int b) const {
+        Xf r;
+        if (b < ND) { r.p = v2(S.xpx[b], S.xpy[b]); r.q.s = S.xs[b]; r.q.c = S.xc[b]; }
+        else { r.p = v2(T.wall_px[b - ND], T.wall_py[b - ND]); r.q.s = 0.0f; r.q.c = 1.0f; }
+        return r;
+    }
+    __device__ V2 center(int b) const { return b < ND ? v2(S.cx[b], S.cy[b]) : v2(T.wall_px[b - ND], T.wall_py[b - ND]); }
+    __device__ V2 lc(int b) const { return v2(T.lcx[b], T.lcy[b]); }
+    __device__ void sync_transform(int b) {   // b2Body::SynchronizeTransform
+        Rot q = rot(S.a[b]);
+        S.xs[b] = q.s; S.xc[b] = q.c;
+        V2 p = vsub(v2(S.cx[b], S.cy[b]), mul_rv(q, lc(b)));
+        S.xpx[b] = p.x; S.xpy[b] = p.y;
+    }
+
+    // ------------------------------------------------------------------ dynamic tree
+    __device__ static float perim(float lx, float ly, float hx, float hy) { float wx = hx - lx; float wy = hy - ly; return 2.0f * (wx + wy); }
+    __device__ int t_alloc() {
+        int id = S.freeList;
+        S.freeList = S.tpar[id];
+        S.tpar[id] = NULLN; S.tc1[id] = NULLN; S.tc2[id] = NULLN; S.th[id] = 0; S.tud[id] = -1;
+        ++S.nodeCount;
+        return id;
+    }
+    __device__ void t_free(int id) { S.tpar[id] = S.freeList; S.th[id] = -1; S.tud[id] = -1; S.freeList = id; --S.nodeCount; }
+    __device__ bool t_leaf(int id) const { return S.tc1[id] == NULLN; }
+    __device__ void t_combine_into(int dst, int a, int b) {
+        S.tlx[dst] = fmin_(S.tlx[a], S.tlx[b]); S.tly[dst] = fmin_(S.tly[a], S.tly[b]);
+        S.thx[dst] = fmax_(S.thx[a], S.thx[b]); S.thy[dst] = fmax_(S.thy[a], S.thy[b]);
+    }
+    __device__ int t_balance(int iA) {
+        if (t_leaf(iA) || S.th[iA] < 2) return iA;
+        int iB = S.tc1[iA], iC = S.tc2[iA];
+        int balance = S.th[iC] - S.th[iB];
+        if (balance > 1) {
+            int iF = S.tc1[iC], iG = S.tc2[iC];
+            S.tc1[iC] = iA; S.tpar[iC] = S.tpar[iA]; S.tpar[iA] = iC;
+            int cp = S.tpar[iC];
+            if (cp != NULLN) { if (S.tc1[cp] == iA) S.tc1[cp] = iC; else S.tc2[cp] = iC; }
+            else S.root = iC;
+            if (S.th[iF] > S.th[iG]) {
+                S.tc2[iC] = iF; S.tc2[iA] = iG; S.tpar[iG] = iA;
+                t_combine_into(iA, iB, iG); t_combine_into(iC, iA, iF);
+                S.th[iA] = 1 + max(S.th[iB], S.th[iG]); S.th[iC] = 1 + max(S.th[iA], S.th[iF]);
+            } else {
+                S.tc2[iC] = iG; S.tc2[iA] = iF; S.tpar[iF] = iA;
+                t_combine_into(iA, iB, iF); t_combine_into(iC, iA, iG);
+                S.th[iA] = 1 + max(S.th[iB], S.th[iF]); S.th[iC] = 1 + max(S.th[iA], S.th[iG]);
+            }
+            return iC;
+        }
+        if (balance < -1) {
+            int iD = S.tc1[iB], iE = S.tc2[iB];
+            S.tc1[iB] = iA; S.tpar[iB] = S.tpar[iA]; S.tpar[iA] = iB;
+            int bp = S.tpar[iB];
+            if (bp != NULLN) { if (S.tc1[bp] == iA) S.tc1[bp] = iB; else S.tc2[bp] = iB; }
+            else S.root = iB;
+            if (S.th[iD] > S.th[iE]) {
+                S.tc2[iB] = iD; S.tc1[iA] = iE; S.tpar[iE] = iA;
+                t_combine_into(iA, iC, iE); t_combine_into(iB, iA, iD);
+                S.th[iA] = 1 + max(S.th[iC], S.th[iE]); S.th[iB] = 1 + max(S.th[iA], S.th[iD]);
+            } else {
+                S.tc2[iB] = iE; S.tc1[iA] = iD; S.tpar[iD] = iA;
+                t_combine_into(iA, iC, iD); t_combine_into(iB, iA, iE);
+                S.th[iA] = 1 + max(S.th[iC], S.th[iD]); S.th[iB] = 1 + max(S.th[iA], S.th[iE]);
+            }
+            return iB;
+        }
+        return iA;
+    }
+    __device__ void t_fix_upwards(int index) {
+        while (index != NULLN) {
+            index = t_balance(index);
+            int c1 = S.tc1[index], c2 = S.tc2[index];
+            S.th[index] = 1 + max(S.th[c1], S.th[c2]);
+            t_combine_into(index, c1, c2);
+            index = S.tpar[index];
+        }
+    }
+    __device__ void t_insert(int leaf) {
+        if (S.root == NULLN) { S.root = leaf; S.tpar[leaf] = NULLN; return; }
+        float llx = S.tlx[leaf], lly = S.tly[leaf], lhx = S.thx[leaf], lhy = S.thy[leaf];
+        int index = S.root;
+        while (!t_leaf(index)) {
+            int c1 = S.tc1[index], c2 = S.tc2[index];
+            float area = perim(S.tlx[index], S.tly[index], S.thx[index], S.thy[index]);
+            float combinedArea = perim(fmin_(S.tlx[index], llx), fmin_(S.tly[index], lly), fmax_(S.thx[index], lhx), fmax_(S.thy[index], lhy));
+            float cost = 2.0f * combinedArea;
+            float inheritanceCost = 2.0f * (combinedArea - area);
+            float cost1, cost2;
+            {
+                float na = perim(fmin_(llx, S.tlx[c1]), fmin_(lly, S.tly[c1]), fmax_(lhx, S.thx[c1]), fmax_(lhy, S.thy[c1]));
+                if (t_leaf(c1)) cost1 = na + inheritanceCost;
+                else { float oa = perim(S.tlx[c1], S.tly[c1], S.thx[c1], S.thy[c1]); cost1 = (na - oa) + inheritanceCost; }
+            }
+            {
+                float na = perim(fmin_(llx, S.tlx[c2]), fmin_(lly, S.tly[c2]), fmax_(lhx, S.thx[c2]), fmax_(lhy, S.thy[c2]));
+                if (t_leaf(c2)) cost2 = na + inheritanceCost;
+                else { float oa = perim(S.tlx[c2], S.tly[c2], S.thx[c2], S.thy[c2]); cost2 = na - oa + inheritanceCost; }
+            }
+            if (cost < cost1 && cost < cost2) break;
+            index = cost1 < cost2 ? c1 : c2;
+        }
+        int sibling = index;
+        int oldParent = S.tpar[sibling];
+        int np = t_alloc();
+        S.tpar[np] = oldParent; S.tud[np] = -1;
+        S.tlx[np] = fmin_(llx, S.tlx[sibling]); S.tly[np] = fmin_(lly, S.tly[sibling]);
+        S.thx[np] = fmax_(lhx, S.thx[sibling]); S.thy[np] = fmax_(lhy, S.thy[sibling]);
+        S.th[np] = S.th[sibling] + 1;
+        if (oldParent != NULLN) { if (S.tc1[oldParent] == sibling) S.tc1[oldParent] = np; else S.tc2[oldParent] = np; }
+        else S.root = np;
+        S.tc1[np] = sibling; S.tc2[np] = leaf; S.tpar[sibling] = np; S.tpar[leaf] = np;
+        t_fix_upwards(S.tpar[leaf]);
+    }
+    __device__ void t_remove(int leaf) {
+        if (leaf == S.root) { S.root = NULLN; return; }
+        int parent = S.tpar[leaf];
+        int grand = S.tpar[parent];
+        int sibling = S.tc1[parent] == leaf ? S.tc2[parent] : S.tc1[parent];
+        if (grand != NULLN) {
+            if (S.tc1[grand] == parent) S.tc1[grand] = sibling; else S.tc2[grand] = sibling;
+            S.tpar[sibling] = grand;
+            t_free(parent);
+            int index = grand;
+            while (index != NULLN) {   // RemoveLeaf: Combine before height (same result as t_fix_upwards)
+                index = t_balance(index);
+                int c1 = S.tc1[index], c2 = S.tc2[index];
+                t_combine_into(index, c1, c2);
+                S.th[index] = 1 + max(S.th[c1], S.th[c2]);
+                index = S.tpar[index];
+            }
+        } else {
+            S.root = sibling; S.tpar[sibling] = NULLN; t_free(parent);
+        }
+    }
+    __device__ void buffer_move(int id) { S.moveBuf[S.moveCount++] = id; }
+    __device__ void unbuffer_move(int id) { for (int i = 0; i < S.moveCount; ++i) if (S.moveBuf[i] == id) S.moveBuf[i] = NULLN; }
+
+    // polygon AABB under a transform (b2PolygonShape::ComputeAABB)
+    __device__ void poly_aabb(const ShapeDef& s, Xf x, float& lx, float& ly, float& hx, float& hy) const {
+        V2 lower = mul_xv(x, s.v[0]), upper = lower;
+        for (int i = 1; i < s.count; ++i) { V2 v = mul_xv(x, s.v[i]); lower = vmin(lower, v); upper = vmax(upper, v); }
+        lx = lower.x - s.radius; ly = lower.y - s.radius; hx = upper.x + s.radius; hy = upper.y + s.radius;
+    }
+    __device__ void create_proxy(int f, Xf x) {
+        float lx, ly, hx, hy;
+        poly_aabb(T.shape[f], x, lx, ly, hx, hy);
+        int id = t_alloc();
+        S.tlx[id] = lx - AABB_EXT; S.tly[id] = ly - AABB_EXT; S.thx[id] = hx + AABB_EXT; S.thy[id] = hy + AABB_EXT;
+        S.tud[id] = f; S.th[id] = 0;
+        t_insert(id);
+        S.proxy[f] = id;
+        buffer_move(id);
+    }
+    __device__ void destroy_proxy(int f) {
+        int id = S.proxy[f];
+        unbuffer_move(id);
+        t_remove(id); t_free(id);
+    }
+    __device__ void move_proxy(int id, float lx, float ly, float hx, float hy, V2 disp) {
+        if (S.tlx[id] <= lx && S.tly[id] <= ly && hx <= S.thx[id] && hy <= S.thy[id]) return;   // Contains
+        t_remove(id);
+        float blx = lx - AABB_EXT, bly = ly - AABB_EXT, bhx = hx + AABB_EXT, bhy = hy + AABB_EXT;
+        V2 d = vmul(AABB_MUL, disp);
+        if (d.x < 0.0f) blx += d.x; else bhx += d.x;
+        if (d.y < 0.0f) bly += d.y; else bhy += d.y;
+        S.tlx[id] = blx; S.tly[id] = bly; S.thx[id] = bhx; S.thy[id] = bhy;
+        t_insert(id);
+        buffer_move(id);
+    }
+    __device__ bool fat_overlap(int a, int b) const {   // b2TestOverlap
+        float d1x = S.tlx[b] - S.thx[a], d1y = S.tly[b] - S.thy[a];
+        float d2x = S.tlx[a] - S.thx[b], d2y = S.tly[a] - S.thy[b];
+        if (d1x > 0.0f || d1y > 0.0f) return false;
+        if (d2x > 0.0f || d2y > 0.0f) return false;
+        return true;
+    }
+    // b2Body::SynchronizeFixtures for a dynamic body, fixtures in fixture-list order (newest first)
+    __device__ void sync_fixtures(int b) {
+        Xf x1; x1.q = rot(S.a0[b]);
+        x1.p = vsub(v2(S.c0x[b], S.c0y[b]), mul_rv(x1.q, lc(b)));
+        Xf x2 = xf(b);
+        for (int k = T.body_nfix[b] - 1; k >= 0; --k) {
+            int f = T.body_fix0[b] + k;
+            float l1x, l1y, h1x, h1y, l2x, l2y, h2x, h2y;
+            poly_aabb(T.shape[f], x1, l1x, l1y, h1x, h1y);
+            poly_aabb(T.shape[f], x2, l2x, l2y, h2x, h2y);
+            V2 disp = vsub(x2.p, x1.p);
+            move_proxy(S.proxy[f], fmin_(l1x, l2x), fmin_(l1y, l2y), fmax_(h1x, h2x), fmax_(h1y, h2y), disp);
+        }
+    }
+
+    // ------------------------------------------------------------------ contacts
+    __device__ void contact_event(int c, int value) {   // ContactDetector (multi_robot_puzzle_00.py:92-111)
+        int bA = T.fix_body[S.cfa[c]], bB = T.fix_body[S.cfb[c]];
+        for (int i = 0; i < NA; ++i) {
+            int ag = NB + i;
+            if (ag == bA || ag == bB) {
+                if (bA == 0 || bB == 0) S.goal_contact[i] = value;
+                if (bA >= ND || bB >= ND) S.wall_contact = value;
+            }
+        }
+    }
+    __device__ void add_pair(int fa, int fb) {   // b2ContactManager::AddPair
+        int bA = T.fix_body[fa], bB = T.fix_body[fb];
+        if (bA == bB) return;
+        for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
+            if ((S.cfa[c] == fa && S.cfb[c] == fb) || (S.cfa[c] == fb && S.cfb[c] == fa)) return;
+        }
+        if (!is_dyn(bA) && !is_dyn(bB)) return;
+        int c = S.cFree;
+        S.cFree = S.cnext[c];
+        S.cfa[c] = fa; S.cfb[c] = fb; S.cflags[c] = CF_ENABLED; S.ctoiCount[c] = 0; S.ctoi[c] = 1.0f;
+        S.cfric[c] = sqrtf(T.fix_friction[fa] * T.fix_friction[fb]);
+        S.mpc[c] = 0;
+        S.cprev[c] = NULLN; S.cnext[c] = S.cHead;
+        if (S.cHead != NULLN) S.cprev[S.cHead] = c;
+        S.cHead = c;
+        ++S.cCount;
+    }
+    __device__ void destroy_contact(int c, bool events) {   // b2ContactManager::Destroy
+        if (events && (S.cflags[c] & CF_TOUCHING)) contact_event(c, 0);
+        int p = S.cprev[c], n = S.cnext[c];
+        if (p != NULLN) S.cnext[p] = n;
+        if (n != NULLN) S.cprev[n] = p;
+        if (S.cHead == c) S.cHead = n;
+        S.cnext[c] = S.cFree; S.cFree = c;
+        --S.cCount;
+    }
+    // b2BroadPhase::UpdatePairs + AddPair: pairs (lower proxy id, higher id) with at least one
+    // moved proxy and overlapping fat AABBs, visited in sorted order == Box2D's sorted pair buffer.
+    __device__ void find_new_contacts() {
+        uint32_t moved = 0;
+        for (int i = 0; i < S.moveCount; ++i) if (S.moveBuf[i] != NULLN) moved |= 1u << S.moveBuf[i];
+        S.moveCount = 0;
+        if (!moved) return;
+        for (int a = 0; a < TREE_N; ++a) {
+            if (S.tud[a] < 0 || !t_leaf(a)) continue;
+            for (int b = a + 1; b < TREE_N; ++b) {
+                if (S.tud[b] < 0 || !t_leaf(b)) continue;
+                if (!(((moved >> a) | (moved >> b)) & 1u)) continue;
+                if (fat_overlap(a, b)) add_pair(S.tud[a], S.tud[b]);
+            }
+        }
+    }
+
+    // ---------------------------------------------------------------- narrow phase (b2CollidePolygons)
+    struct ClipV { V2 v; uint32_t id; };
+    __device__ static uint32_t cf_make(int iA, int iB, int tA, int tB) {
+        return (uint32_t)(uint8_t)iA | ((uint32_t)(uint8_t)iB << 8) | ((uint32_t)(uint8_t)tA << 16) | ((uint32_t)(uint8_t)tB << 24);
+    }
+    __device__ static float find_max_separation(int& edge, const ShapeDef& p1, Xf x1, const ShapeDef& p2, Xf x2) {
+        Xf x = mulT_xx(x2, x1);
+        int best = 0; float maxSep = -FLT_MAXV;
+        for (int i = 0; i < p1.count; ++i) {
+            V2 n = mul_rv(x.q, p1.n[i]);
+            V2 v1 = mul_xv(x, p1.v[i]);
+            float si = FLT_MAXV;
+            for (int j = 0; j < p2.count; ++j) { float sij = vdot(n, vsub(p2.v[j], v1)); if (sij < si) si = sij; }
+            if (si > maxSep) { maxSep = si; best = i; }
+        }
+        edge = best;
+        return maxSep;
+    }
+    __device__ static int clip(ClipV out[2], const ClipV in[2], V2 normal, float offset, int vertexIndexA) {
+        int numOut = 0;
+        float d0 = vdot(normal, in[0].v) - offset;
+        float d1 = vdot(normal, in[1].v) - offset;
+        if (d0 <= 0.0f) out[numOut++] = in[0];
+        if (d1 <= 0.0f) out[numOut++] = in[1];
+        if (d0 * d1 < 0.0f) {
+            float interp = d0 / (d0 - d1);
+            out[numOut].v = vadd(in[0].v, vmul(interp, vsub(in[1].v, in[0].v)));
+            out[numOut].id = cf_make(vertexIndexA, (int)((in[0].id >> 8) & 0xff), 0, 1);
+            ++numOut;
+        }
+        return numOut;
+    }
+    // writes the manifold of slot c
+    __device__ void collide_polygons(int c, const ShapeDef& pA, Xf xA, const ShapeDef& pB, Xf xB) {
+        S.mpc[c] = 0;
+        float totalRadius = pA.radius + pB.radius;
+        int edgeA = 0;
+        float sepA = find_max_separation(edgeA, pA, xA, pB, xB);
+        if (sepA > totalRadius) return;
+        int edgeB = 0;
+        float sepB = find_max_separation(edgeB, pB, xB, pA, xA);
+        if (sepB > totalRadius) return;
+        const float k_tol = 0.1f * LINEAR_SLOP;
+        bool flip = sepB > sepA + k_tol;
+        const ShapeDef& p1 = flip ? pB : pA;
+        const ShapeDef& p2 = flip ? pA : pB;
+        Xf x1 = flip ? xB : xA, x2 = flip ? xA : xB;
+        int edge1 = flip ? edgeB : edgeA;
+        S.mtype[c] = flip ? MT_FACEB : MT_FACEA;
+        // incident edge
+        ClipV inc[2];
+        {
+            V2 normal1 = mulT_rv(x2.q, mul_rv(x1.q, p1.n[edge1]));
+            int index = 0; float minDot = FLT_MAXV;
+            for (int i = 0; i < p2.count; ++i) { float d = vdot(normal1, p2.n[i]); if (d < minDot) { minDot = d; index = i; } }
+            int i1 = index, i2 = i1 + 1 < p2.count ? i1 + 1 : 0;
+            inc[0].v = mul_xv(x2, p2.v[i1]); inc[0].id = cf_make(edge1, i1, 1, 0);
+            inc[1].v = mul_xv(x2, p2.v[i2]); inc[1].id = cf_make(edge1, i2, 1, 0);
+        }
+        int iv1 = edge1, iv2 = edge1 + 1 < p1.count ? edge1 + 1 : 0;
+        V2 v11 = p1.v[iv1], v12 = p1.v[iv2];
+        V2 localTangent = vsub(v12, v11);
+        vnormalize(localTangent);
+        V2 localNormal = vcross_vs(localTangent, 1.0f);
+        V2 planePoint = vmul(0.5f, vadd(v11, v12));
+        V2 tangent = mul_rv(x1.q, localTangent);
+        V2 normal = vcross_vs(tangent, 1.0f);
+        v11 = mul_xv(x1, v11); v12 = mul_xv(x1, v12);
+        float frontOffset = vdot(normal, v11);
+        float side1 = -vdot(tangent, v11) + totalRadius;
+        float side2 = vdot(tangent, v12) + totalRadius;
+        ClipV cp1[2], cp2[2];
+        if (clip(cp1, inc, vneg(tangent), side1, iv1) < 2) return;
+        if (clip(cp2, cp1, tangent, side2, iv2) < 2) return;
+        S.mlnx[c] = localNormal.x; S.mlny[c] = localNormal.y;
+        S.mlpx[c] = planePoint.x; S.mlpy[c] = planePoint.y;
+        int pc = 0;
+        for (int i = 0; i < 2; ++i) {
+            float sep = vdot(normal, cp2[i].v) - frontOffset;
+            if (sep <= totalRadius) {
+                V2 lp = mulT_xv(x2, cp2[i].v);
+                uint32_t id = cp2[i].id;
+                if (flip) {
+                    uint32_t a0 = id & 0xff, b0 = (id >> 8) & 0xff, ta = (id >> 16) & 0xff, tb = (id >> 24) & 0xff;
+                    id = b0 | (a0 << 8) | (tb << 16) | (ta << 24);
+                }
+                S.mpx[pc][c] = lp.x; S.mpy[pc][c] = lp.y; S.mid[pc][c] = id;
+                ++pc;
+            }
+        }
+        S.mpc[c] = pc;
+    }
+    // b2Contact::Update
+    __device__ void contact_update(int c) {
+        int oldCount = S.mpc[c];
+        uint32_t oid0 = S.mid[0][c], oid1 = S.mid[1][c];
+        float on0 = S.mni[0][c], on1 = S.mni[1][c], ot0 = S.mti[0][c], ot1 = S.mti[1][c];
+        S.cflags[c] |= CF_ENABLED;
+        bool wasTouching = (S.cflags[c] & CF_TOUCHING) != 0;
+        int fa = S.cfa[c], fb = S.cfb[c];
+        collide_polygons(c, T.shape[fa], xf(T.fix_body[fa]), T.shape[fb], xf(T.fix_body[fb]));
+        bool touching = S.mpc[c] > 0;
+        for (int i = 0; i < S.mpc[c]; ++i) {
+            uint32_t id2 = S.mid[i][c];
+            float ni = 0.0f, ti = 0.0f;
+            if (oldCount > 0 && oid0 == id2) { ni = on0; ti = ot0; }
+            else if (oldCount > 1 && oid1 == id2) { ni = on1; ti = ot1; }
+            S.mni[i][c] = ni; S.mti[i][c] = ti;
+        }
+        if (touching) S.cflags[c] |= CF_TOUCHING; else S.cflags[c] &= ~CF_TOUCHING;
+        if (!wasTouching && touching) contact_event(c, 1);
+        if (wasTouching && !touching) contact_event(c, 0);
+    }
+    __device__ void collide() {   // b2ContactManager::Collide
+        int c = S.cHead;
+        while (c != NULLN) {
+            int next = S.cnext[c];
+            if (!fat_overlap(S.proxy[S.cfa[c]], S.proxy[S.cfb[c]])) { destroy_contact(c, true); c = next; continue; }
+            contact_update(c);
+            c = next;
+        }
+    }
+
+    // ---------------------------------------------------------------- contact solver
+    struct VC {
+        float rAx[2], rAy[2], rBx[2], rBy[2], ni[2], ti[2], nmass[2], tmass[2], vbias[2];
+        float nx, ny, nm0, nm1, nm2, nm3, k0, k1, k2, k3;
+        float mA, mB, iA, iB, friction, restitution;
+        int iaI, ibI, pointCount, slot;
+    };
+    struct PC {
+        float lpx[2], lpy[2], lnx, lny, lpx0, lpy0;
+        float mA, mB, iA, iB, lcAx, lcAy, lcBx, lcBy, rA, rB;
+        int iaI, ibI, type, pointCount;
+    };
+    struct Isl {
+        int bodies[NBODY];
+        int contacts[C];
+        float pcx[NBODY], pcy[NBODY], pa[NBODY], vvx[NBODY], vvy[NBODY], vw[NBODY];
+        int nb, nc;
+        int index[NBODY];   // body -> island index
+    };
+    __device__ float body_invMass(int b) const { return T.invMass[b]; }
+    __device__ float body_invI(int b) const { return T.invI[b]; }
+
+    __device__ void solver_init(Isl& is, VC* vcs, PC* pcs, bool warm, float dtRatio) {
+        for (int i = 0; i < is.nc; ++i) {
+            int c = is.contacts[i];
+            int fa = S.cfa[c], fb = S.cfb[c];
+            int bA = T.fix_body[fa], bB = T.fix_body[fb];
+            int pcount = S.mpc[c];
+            VC& vc = vcs[i];
+            vc.friction = S.cfric[c]; vc.restitution = fmax_(T.fix_restitution[fa], T.fix_restitution[fb]);
+            vc.iaI = is.index[bA]; vc.ibI = is.index[bB];
+            vc.mA = T.invMass[bA]; vc.mB = T.invMass[bB]; vc.iA = T.invI[bA]; vc.iB = T.invI[bB];
+            vc.slot = c; vc.pointCount = pcount;
+            vc.k0 = vc.k1 = vc.k2 = vc.k3 = 0.0f; vc.nm0 = vc.nm1 = vc.nm2 = vc.nm3 = 0.0f;
+            PC& pc = pcs[i];
+            pc.iaI = vc.iaI; pc.ibI = vc.ibI;
+            pc.mA = vc.mA; pc.mB = vc.mB; pc.iA = vc.iA; pc.iB = vc.iB;
+            pc.lcAx = T.lcx[bA]; pc.lcAy = T.lcy[bA]; pc.lcBx = T.lcx[bB]; pc.lcBy = T.lcy[bB];
+            pc.lnx = S.mlnx[c]; pc.lny = S.mlny[c]; pc.lpx0 = S.mlpx[c]; pc.lpy0 = S.mlpy[c];
+            pc.pointCount = pcount; pc.rA = T.shape[fa].radius; pc.rB = T.shape[fb].radius; pc.type = S.mtype[c];
+            for (int j = 0; j < pcount; ++j) {
+                if (warm) { vc.ni[j] = dtRatio * S.mni[j][c]; vc.ti[j] = dtRatio * S.mti[j][c]; }
+                else { vc.ni[j] = 0.0f; vc.ti[j] = 0.0f; }
+                vc.rAx[j] = vc.rAy[j] = vc.rBx[j] = vc.rBy[j] = 0.0f;
+                vc.nmass[j] = 0.0f; vc.tmass[j] = 0.0f; vc.vbias[j] = 0.0f;
+                pc.lpx[j] = S.mpx[j][c]; pc.lpy[j] = S.mpy[j][c];
+            }
+        }
+    }
+    __device__ void solver_init_velocity(Isl& is, VC* vcs, PC* pcs) {
+        for (int i = 0; i < is.nc; ++i) {
+            VC& vc = vcs[i]; PC& pc = pcs[i];
+            int c = vc.slot;
+            int ia = vc.iaI, ib = vc.ibI;
+            float mA = vc.mA, mB = vc.mB, iA = vc.iA, iB = vc.iB;
+            V2 cA = v2(is.pcx[ia], is.pcy[ia]); float aA = is.pa[ia];
+            V2 vA = v2(is.vvx[ia], is.vvy[ia]); float wA = is.vw[ia];
+            V2 cB = v2(is.pcx[ib], is.pcy[ib]); float aB = is.pa[ib];
+            V2 vB = v2(is.vvx[ib], is.vvy[ib]); float wB = is.vw[ib];
+            Xf xA, xB;
+            xA.q = rot(aA); xB.q = rot(aB);
+            xA.p = vsub(cA, mul_rv(xA.q, v2(pc.lcAx, pc.lcAy)));
+            xB.p = vsub(cB, mul_rv(xB.q, v2(pc.lcBx, pc.lcBy)));
+            // b2WorldManifold::Initialize
+            V2 normal; V2 pts[2];
+            int mpcount = S.mpc[c];
+            if (S.mtype[c] == MT_FACEA) {
+                normal = mul_rv(xA.q, v2(S.mlnx[c], S.mlny[c]));
+                V2 planePoint = mul_xv(xA, v2(S.mlpx[c], S.mlpy[c]));
+                for (int j = 0; j < mpcount; ++j) {
+                    V2 clipPoint = mul_xv(xB, v2(S.mpx[j][c], S.mpy[j][c]));
+                    V2 pA = vadd(clipPoint, vmul(pc.rA - vdot(vsub(clipPoint, planePoint), normal), normal));
+                    V2 pB = vsub(clipPoint, vmul(pc.rB, normal));
+                    pts[j] = vmul(0.5f, vadd(pA, pB));
+                }
+            } else {
+                normal = mul_rv(xB.q, v2(S.mlnx[c], S.mlny[c]));
+                V2 planePoint = mul_xv(xB, v2(S.mlpx[c], S.mlpy[c]));
+                for (int j = 0; j < mpcount; ++j) {
+                    V2 clipPoint = mul_xv(xA, v2(S.mpx[j][c], S.mpy[j][c]));
+                    V2 pB = vadd(clipPoint, vmul(pc.rB - vdot(vsub(clipPoint, planePoint), normal), normal));
+                    V2 pA = vsub(clipPoint, vmul(pc.rA, normal));
+                    pts[j] = vmul(0.5f, vadd(pA, pB));
+                }
+                normal = vneg(normal);
+            }
+            vc.nx = normal.x; vc.ny = normal.y;
+            for (int j = 0; j < vc.pointCount; ++j) {
+                V2 rA = vsub(pts[j], cA), rB = vsub(pts[j], cB);
+                vc.rAx[j] = rA.x; vc.rAy[j] = rA.y; vc.rBx[j] = rB.x; vc.rBy[j] = rB.y;
+                float rnA = vcross(rA, normal), rnB = vcross(rB, normal);
+                float kNormal = mA + mB + iA * rnA * rnA + iB * rnB * rnB;
+                vc.nmass[j] = kNormal > 0.0f ? 1.0f / kNormal : 0.0f;
+                V2 tangent = vcross_vs(normal, 1.0f);
+                float rtA = vcross(rA, tangent), rtB = vcross(rB, tangent);
+                float kTangent = mA + mB + iA * rtA * rtA + iB * rtB * rtB;
+                vc.tmass[j] = kTangent > 0.0f ? 1.0f / kTangent : 0.0f;
+                vc.vbias[j] = 0.0f;
+                V2 dvr = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
+                float vRel = vdot(normal, dvr);
+                if (vRel < -VELOCITY_THRESHOLD) vc.vbias[j] = -vc.restitution * vRel;
+            }
+            if (vc.pointCount == 2) {
+                float rn1A = vcross(v2(vc.rAx[0], vc.rAy[0]), normal), rn1B = vcross(v2(vc.rBx[0], vc.rBy[0]), normal);
+                float rn2A = vcross(v2(vc.rAx[1], vc.rAy[1]), normal), rn2B = vcross(v2(vc.rBx[1], vc.rBy[1]), normal);
+                float k11 = mA + mB + iA * rn1A * rn1A + iB * rn1B * rn1B;
+                float k22 = mA + mB + iA * rn2A * rn2A + iB * rn2B * rn2B;
+                float k12 = mA + mB + iA * rn1A * rn2A + iB * rn1B * rn2B;
+                const float k_maxConditionNumber = 1000.0f;
+                if (k11 * k11 < k_maxConditionNumber * (k11 * k22 - k12 * k12)) {
+                    vc.k0 = k11; vc.k1 = k12; vc.k2 = k12; vc.k3 = k22;
+                    float a = vc.k0, b = vc.k2, cc = vc.k1, d = vc.k3;
+                    float det = a * d - b * cc;
+                    if (det != 0.0f) det = 1.0f / det;
+                    vc.nm0 = det * d; vc.nm2 = -det * b; vc.nm1 = -det * cc; vc.nm3 = det * a;
+                } else {
+                    vc.pointCount = 1;
+                }
+            }
+        }
+    }
+    __device__ void solver_warm_start(Isl& is, VC* vcs) {
+        for (int i = 0; i < is.nc; ++i) {
+            VC& vc = vcs[i];
+            int ia = vc.iaI, ib = vc.ibI;
+            V2 vA = v2(is.vvx[ia], is.vvy[ia]); float wA = is.vw[ia];
+            V2 vB = v2(is.vvx[ib], is.vvy[ib]); float wB = is.vw[ib];
+            V2 normal = v2(vc.nx, vc.ny), tangent = vcross_vs(normal, 1.0f);
+            for (int j = 0; j < vc.pointCount; ++j) {
+                V2 P = vadd(vmul(vc.ni[j], normal), vmul(vc.ti[j], tangent));
+                wA -= vc.iA * vcross(v2(vc.rAx[j], vc.rAy[j]), P);
+                vA = vsub(vA, vmul(vc.mA, P));
+                wB += vc.iB * vcross(v2(vc.rBx[j], vc.rBy[j]), P);
+                vB = vadd(vB, vmul(vc.mB, P));
+            }
+            is.vvx[ia] = vA.x; is.vvy[ia] = vA.y; is.vw[ia] = wA;
+            is.vvx[ib] = vB.x; is.vvy[ib] = vB.y; is.vw[ib] = wB;
+        }
+    }
+    __device__ void solver_velocity(Isl& is, VC* vcs) {   // b2ContactSolver::SolveVelocityConstraints
+        for (int i = 0; i < is.nc; ++i) {
+            VC& vc = vcs[i];
+            int ia = vc.iaI, ib = vc.ibI;
+            float mA = vc.mA, iA = vc.iA, mB = vc.mB, iB = vc.iB;
+            V2 vA = v2(is.vvx[ia], is.vvy[ia]); float wA = is.vw[ia];
+            V2 vB = v2(is.vvx[ib], is.vvy[ib]); float wB = is.vw[ib];
+            V2 normal = v2(vc.nx, vc.ny), tangent = vcross_vs(normal, 1.0f);
+            float friction = vc.friction;
+            for (int j = 0; j < vc.pointCount; ++j) {
+                V2 rA = v2(vc.rAx[j], vc.rAy[j]), rB = v2(vc.rBx[j], vc.rBy[j]);
+                V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
+                float vt = vdot(dv, tangent) - 0.0f;
+                float lambda = vc.tmass[j] * (-vt);
+                float maxFriction = friction * vc.ni[j];
+                float newImpulse = fclamp(vc.ti[j] + lambda, -maxFriction, maxFriction);
+                lambda = newImpulse - vc.ti[j];
+                vc.ti[j] = newImpulse;
+                V2 P = vmul(lambda, tangent);
+                vA = vsub(vA, vmul(mA, P));
+                wA -= iA * vcross(rA, P);
+                vB = vadd(vB, vmul(mB, P));
+                wB += iB * vcross(rB, P);
+            }
+            if (vc.pointCount == 1) {
+                V2 rA = v2(vc.rAx[0], vc.rAy[0]), rB = v2(vc.rBx[0], vc.rBy[0]);
+                V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
+                float vn = vdot(dv, normal);
+                float lambda = -vc.nmass[0] * (vn - vc.vbias[0]);
+                float newImpulse = fmax_(vc.ni[0] + lambda, 0.0f);
+                lambda = newImpulse - vc.ni[0];
+                vc.ni[0] = newImpulse;
+                V2 P = vmul(lambda, normal);
+                vA = vsub(vA, vmul(mA, P));
+                wA -= iA * vcross(rA, P);
+                vB = vadd(vB, vmul(mB, P));
+                wB += iB * vcross(rB, P);
+            } else {
+                V2 r1A = v2(vc.rAx[0], vc.rAy[0]), r1B = v2(vc.rBx[0], vc.rBy[0]);
+                V2 r2A = v2(vc.rAx[1], vc.rAy[1]), r2B = v2(vc.rBx[1], vc.rBy[1]);
+                V2 a = v2(vc.ni[0], vc.ni[1]);
+                V2 dv1 = vsub(vsub(vadd(vB, vcross_sv(wB, r1B)), vA), vcross_sv(wA, r1A));
+                V2 dv2 = vsub(vsub(vadd(vB, vcross_sv(wB, r2B)), vA), vcross_sv(wA, r2A));
+                float vn1 = vdot(dv1, normal), vn2 = vdot(dv2, normal);
+                V2 b = v2(vn1 - vc.vbias[0], vn2 - vc.vbias[1]);
+                b = vsub(b, v2(vc.k0 * a.x + vc.k2 * a.y, vc.k1 * a.x + vc.k3 * a.y));
+                V2 x;
+                bool ok = false;
+                x = vneg(v2(vc.nm0 * b.x + vc.nm2 * b.y, vc.nm1 * b.x + vc.nm3 * b.y));
+                if (x.x >= 0.0f && x.y >= 0.0f) ok = true;
+                if (!ok) {
+                    x.x = -vc.nmass[0] * b.x; x.y = 0.0f;
+                    vn2 = vc.k1 * x.x + b.y;
+                    if (x.x >= 0.0f && vn2 >= 0.0f) ok = true;
+                }
+                if (!ok) {
+                    x.x = 0.0f; x.y = -vc.nmass[1] * b.y;
+                    vn1 = vc.k2 * x.y + b.x;
+                    if (x.y >= 0.0f && vn1 >= 0.0f) ok = true;
+                }
+                if (!ok) {
+                    x.x = 0.0f; x.y = 0.0f; vn1 = b.x; vn2 = b.y;
+                    if (vn1 >= 0.0f && vn2 >= 0.0f) ok = true;
+                }
+                if (ok) {
+                    V2 d = vsub(x, a);
+                    V2 P1 = vmul(d.x, normal), P2 = vmul(d.y, normal);
+                    vA = vsub(vA, vmul(mA, vadd(P1, P2)));
+                    wA -= iA * (vcross(r1A, P1) + vcross(r2A, P2));
+                    vB = vadd(vB, vmul(mB, vadd(P1, P2)));
+                    wB += iB * (vcross(r1B, P1) + vcross(r2B, P2));
+                    vc.ni[0] = x.x; vc.ni[1] = x.y;
+                }
+            }
+            is.vvx[ia] = vA.x; is.vvy[ia] = vA.y; is.vw[ia] = wA;
+            is.vvx[ib] = vB.x; is.vvy[ib] = vB.y; is.vw[ib] = wB;
+        }
+    }
+    __device__ void solver_store(Isl& is, VC* vcs) {
+        for (int i = 0; i < is.nc; ++i) {
+            VC& vc = vcs[i];
+            for (int j = 0; j < vc.pointCount; ++j) { S.mni[j][vc.slot] = vc.ni[j]; S.mti[j][vc.slot] = vc.ti[j]; }
+        }
+    }
+    __device__ bool solver_position(Isl& is, PC* pcs, bool toi, int toiA, int toiB) {
+        float minSep = 0.0f;
+        for (int i = 0; i < is.nc; ++i) {
+            PC& pc = pcs[i];
+            int ia = pc.iaI, ib = pc.ibI;
+            float mA, iA, mB, iB;
+            if (!toi) { mA = pc.mA; iA = pc.iA; mB = pc.mB; iB = pc.iB; }
+            else {
+                mA = 0.0f; iA = 0.0f; if (ia == toiA || ia == toiB) { mA = pc.mA; iA = pc.iA; }
+                mB = 0.0f; iB = 0.0f; if (ib == toiA || ib == toiB) { mB = pc.mB; iB = pc.iB; }
+            }
+            V2 cA = v2(is.pcx[ia], is.pcy[ia]); float aA = is.pa[ia];
+            V2 cB = v2(is.pcx[ib], is.pcy[ib]); float aB = is.pa[ib];
+            for (int j = 0; j < pc.pointCount; ++j) {
+                Xf xA, xB;
+                xA.q = rot(aA); xB.q = rot(aB);
+                xA.p = vsub(cA, mul_rv(xA.q, v2(pc.lcAx, pc.lcAy)));
+                xB.p = vsub(cB, mul_rv(xB.q, v2(pc.lcBx, pc.lcBy)));
+                V2 normal, point; float sep;
+                if (pc.type == MT_FACEA) {
+                    normal = mul_rv(xA.q, v2(pc.lnx, pc.lny));
+                    V2 planePoint = mul_xv(xA, v2(pc.lpx0, pc.lpy0));
+                    V2 clipPoint = mul_xv(xB, v2(pc.lpx[j], pc.lpy[j]));
+                    sep = vdot(vsub(clipPoint, planePoint), normal) - pc.rA - pc.rB;
+                    point = clipPoint;
+                } else {
+                    normal = mul_rv(xB.q, v2(pc.lnx, pc.lny));
+                    V2 planePoint = mul_xv(xB, v2(pc.lpx0, pc.lpy0));
+                    V2 clipPoint = mul_xv(xA, v2(pc.lpx[j], pc.lpy[j]));
+                    sep = vdot(vsub(clipPoint, planePoint), normal) - pc.rA - pc.rB;
+                    point = clipPoint;
+                    normal = vneg(normal);
+                }
+                V2 rA = vsub(point, cA), rB = vsub(point, cB);
+                minSep = fmin_(minSep, sep);
+                float Cc = fclamp((toi ? TOI_BAUMGARTE : BAUMGARTE) * (sep + LINEAR_SLOP), -MAX_LINEAR_CORRECTION, 0.0f);
+                float rnA = vcross(rA, normal), rnB = vcross(rB, normal);
+                float K = mA + mB + iA * rnA * rnA + iB * rnB * rnB;
+                float impulse = K > 0.0f ? -Cc / K : 0.0f;
+                V2 Pv = vmul(impulse, normal);
+                cA = vsub(cA, vmul(mA, Pv));
+                aA -= iA * vcross(rA, Pv);
+                cB = vadd(cB, vmul(mB, Pv));
+                aB += iB * vcross(rB, Pv);
+            }
+            is.pcx[ia] = cA.x; is.pcy[ia] = cA.y; is.pa[ia] = aA;
+            is.pcx[ib] = cB.x; is.pcy[ib] = cB.y; is.pa[ib] = aB;
+        }
+        return toi ? (minSep >= -1.5f * LINEAR_SLOP) : (minSep >= -3.0f * LINEAR_SLOP);
+    }
+    __device__ void integrate_positions(Isl& is, float h) {
+        for (int i = 0; i < is.nb; ++i) {
+            V2 c = v2(is.pcx[i], is.pcy[i]); float a = is.pa[i];
+            V2 v = v2(is.vvx[i], is.vvy[i]); float w = is.vw[i];
+            V2 translation = vmul(h, v);
+            if (vdot(translation, translation) > MAX_TRANSLATION_SQ) {
+                float ratio = MAX_TRANSLATION / vlen(translation);
+                v.x *= ratio; v.y *= ratio;
+            }
+            float rotation = h * w;
+            if (rotation * rotation > MAX_ROTATION_SQ) {
+                float ratio = MAX_ROTATION / fabsf(rotation);
+                w *= ratio;
+            }
+            c = vadd(c, vmul(h, v));
+            a += h * w;
+            is.pcx[i] = c.x; is.pcy[i] = c.y; is.pa[i] = a;
+            is.vvx[i] = v.x; is.vvy[i] = v.y; is.vw[i] = w;
+        }
+    }
+    __device__ void island_add_body(Isl& is, int b) { is.index[b] = is.nb; is.bodies[is.nb++] = b; }
+
+    // b2Island::Solve (discrete step of one island)
+    __device__ void island_solve(Isl& is, float h, float dtRatio, VC* vcs, PC* pcs) {
+        for (int i = 0; i < is.nb; ++i) {
+            int b = is.bodies[i];
+            if (is_dyn(b)) {
+                V2 c = v2(S.cx[b], S.cy[b]); float a = S.a[b];
+                V2 v = v2(S.vx[b], S.vy[b]); float w = S.w[b];
+                S.c0x[b] = S.cx[b]; S.c0y[b] = S.cy[b]; S.a0[b] = S.a[b];
+                V2 g = v2(1.0f * 0.0f, 1.0f * 0.0f);   // gravityScale * gravity (0,0)
+                V2 acc = vadd(g, vmul(T.invMass[b], v2(S.fx[b], S.fy[b])));
+                v = vadd(v, vmul(h, acc));
+                w += h * T.invI[b] * S.tq[b];
+                { float s = 1.0f / (1.0f + h * T.linDamp[b]); v.x *= s; v.y *= s; }
+                w *= 1.0f / (1.0f + h * T.angDamp[b]);
+                is.pcx[i] = c.x; is.pcy[i] = c.y; is.pa[i] = a; is.vvx[i] = v.x; is.vvy[i] = v.y; is.vw[i] = w;
+            } else {
+                V2 c = center(b);
+                is.pcx[i] = c.x; is.pcy[i] = c.y; is.pa[i] = 0.0f; is.vvx[i] = 0.0f; is.vvy[i] = 0.0f; is.vw[i] = 0.0f;
+            }
+        }
+        solver_init(is, vcs, pcs, true, dtRatio);
+        solver_init_velocity(is, vcs, pcs);
+        solver_warm_start(is, vcs);
+        for (int it = 0; it < 180; ++it) solver_velocity(is, vcs);
+        solver_store(is, vcs);
+        integrate_positions(is, h);
+        for (int it = 0; it < 60; ++it) {
+            ++S.posIters;
+            if (solver_position(is, pcs, false, -1, -1)) break;
+        }
+        for (int i = 0; i < is.nb; ++i) {
+            int b = is.bodies[i];
+            if (!is_dyn(b)) continue;   // static bodies are unchanged by construction (v = 0, invMass = 0)
+            S.cx[b] = is.pcx[i]; S.cy[b] = is.pcy[i]; S.a[b] = is.pa[i];
+            S.vx[b] = is.vvx[i]; S.vy[b] = is.vvy[i]; S.w[b] = is.vw[i];
+            sync_transform(b);
+        }
+    }
+
+    // b2World::Solve
+    __device__ void solve(float h, float dtRatio) {
+        Isl is;
+        VC vcs[C];
+        PC pcs[C];
+        bool bflag[NBODY];
+        for (int b = 0; b < NBODY; ++b) bflag[b] = false;
+        for (int c = S.cHead; c != NULLN; c = S.cnext[c]) S.cflags[c] &= ~CF_ISLAND;
+        int stack[NBODY];
+        // body list = reverse creation order: walls (static, never seeds), agents, blocks
+        for (int seed = ND - 1; seed >= 0; --seed) {
+            if (bflag[seed]) continue;
+            is.nb = 0; is.nc = 0;
+            int sc = 0;
+            stack[sc++] = seed; bflag[seed] = true;
+            while (sc > 0) {
+                int b = stack[--sc];
+                island_add_body(is, b);
+                if (!is_dyn(b)) continue;
+                for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
+                    int bA = T.fix_body[S.cfa[c]], bB = T.fix_body[S.cfb[c]];
+                    if (bA != b && bB != b) continue;
+                    if (S.cflags[c] & CF_ISLAND) continue;
+                    if ((S.cflags[c] & CF_ENABLED) == 0 || (S.cflags[c] & CF_TOUCHING) == 0) continue;
+                    is.contacts[is.nc++] = c;
+                    S.cflags[c] |= CF_ISLAND;
+                    int other = bA == b ? bB : bA;
+                    if (bflag[other]) continue;
+                    stack[sc++] = other; bflag[other] = true;
+                }
+            }
+            island_solve(is, h, dtRatio, vcs, pcs);
+            for (int i = 0; i < is.nb; ++i) if (!is_dyn(is.bodies[i])) bflag[is.bodies[i]] = false;
+        }
+        for (int b = ND - 1; b >= 0; --b) if (bflag[b]) sync_fixtures(b);
+        find_new_contacts();
+    }
+
+    // ---------------------------------------------------------------- TOI
+    struct SweepV { float lcx, lcy, c0x, c0y, cx, cy, a0, a, alpha0; };
+    __device__ SweepV sweep(int b, const float* salpha0) const {
+        SweepV s;
+        if (b < ND) { s.lcx = T.lcx[b]; s.lcy = T.lcy[b]; s.c0x = S.c0x[b]; s.c0y = S.c0y[b]; s.cx = S.cx[b]; s.cy = S.cy[b]; s.a0 = S.a0[b]; s.a = S.a[b]; s.alpha0 = S.alpha0[b]; }
+        else { s.lcx = 0.0f; s.lcy = 0.0f; s.c0x = s.cx = T.wall_px[b - ND]; s.c0y = s.cy = T.wall_py[b - ND]; s.a0 = s.a = 0.0f; s.alpha0 = salpha0[b - ND]; }
+        return s;
+    }
+    __device__ static Xf sweep_xf(const SweepV& s, float beta) {
+        Xf x;
+        x.p = vadd(vmul(1.0f - beta, v2(s.c0x, s.c0y)), vmul(beta, v2(s.cx, s.cy)));
+        float angle = (1.0f - beta) * s.a0 + beta * s.a;
+        x.q = rot(angle);
+        x.p = vsub(x.p, mul_rv(x.q, v2(s.lcx, s.lcy)));
+        return x;
+    }
+    __device__ static void sweep_advance(SweepV& s, float alpha) {
+        float beta = (alpha - s.alpha0) / (1.0f - s.alpha0);
+        V2 c0 = vadd(v2(s.c0x, s.c0y), vmul(beta, vsub(v2(s.cx, s.cy), v2(s.c0x, s.c0y))));
+        s.c0x = c0.x; s.c0y = c0.y;
+        s.a0 += beta * (s.a - s.a0);
+        s.alpha0 = alpha;
+    }
+    __device__ void sweep_store(int b, const SweepV& s, float* salpha0) {
+        if (b < ND) { S.c0x[b] = s.c0x; S.c0y[b] = s.c0y; S.cx[b] = s.cx; S.cy[b] = s.cy; S.a0[b] = s.a0; S.a[b] = s.a; S.alpha0[b] = s.alpha0; }
+        else salpha0[b - ND] = s.alpha0;
+    }
+    __device__ void body_advance(int b, float alpha, float* salpha0) {   // b2Body::Advance
+        SweepV s = sweep(b, salpha0);
+        sweep_advance(s, alpha);
+        s.cx = s.c0x; s.cy = s.c0y; s.a = s.a0;
+        sweep_store(b, s, salpha0);
+        if (b < ND) sync_transform(b);
+    }
+
+    struct DProxy { const V2* v; int count; float radius; };
+    __device__ static int support(const DProxy& p, V2 d) {
+        int best = 0; float bv = vdot(p.v[0], d);
+        for (int i = 1; i < p.count; ++i) { float val = vdot(p.v[i], d); if (val > bv) { best = i; bv = val; } }
+        return best;
+    }
+    struct SVert { V2 wA, wB, w; float a; int iA, iB; };
+    struct Simplex { SVert v[3]; int count; };
+    struct SCache { float metric; int count; int iA[3], iB[3]; };
+    __device__ static float s_metric(const Simplex& s) {
+        if (s.count == 2) return vlen(vsub(s.v[0].w, s.v[1].w));
+        if (s.count == 3) return vcross(vsub(s.v[1].w, s.v[0].w), vsub(s.v[2].w, s.v[0].w));
+        return 0.0f;
+    }
+    __device__ static void s_solve2(Simplex& s) {
+        V2 w1 = s.v[0].w, w2 = s.v[1].w, e12 = vsub(w2, w1);
+        float d12_2 = -vdot(w1, e12);
+        if (d12_2 <= 0.0f) { s.v[0].a = 1.0f; s.count = 1; return; }
+        float d12_1 = vdot(w2, e12);
+        if (d12_1 <= 0.0f) { s.v[1].a = 1.0f; s.count = 1; s.v[0] = s.v[1]; return; }
+        float inv = 1.0f / (d12_1 + d12_2);
+        s.v[0].a = d12_1 * inv; s.v[1].a = d12_2 * inv; s.count = 2;
+    }
+    __device__ static void s_solve3(Simplex& s) {
+        V2 w1 = s.v[0].w, w2 = s.v[1].w, w3 = s.v[2].w;
+        V2 e12 = vsub(w2, w1);
+        float d12_1 = vdot(w2, e12), d12_2 = -vdot(w1, e12);
+        V2 e13 = vsub(w3, w1);
+        float d13_1 = vdot(w3, e13), d13_2 = -vdot(w1, e13);
+        V2 e23 = vsub(w3, w2);
+        float d23_1 = vdot(w3, e23), d23_2 = -vdot(w2, e23);
+        float n123 = vcross(e12, e13);
+        float d123_1 = n123 * vcross(w2, w3), d123_2 = n123 * vcross(w3, w1), d123_3 = n123 * vcross(w1, w2);
+        if (d12_2 <= 0.0f && d13_2 <= 0.0f) { s.v[0].a = 1.0f; s.count = 1; return; }
+        if (d12_1 > 0.0f && d12_2 > 0.0f && d123_3 <= 0.0f) { float inv = 1.0f / (d12_1 + d12_2); s.v[0].a = d12_1 * inv; s.v[1].a = d12_2 * inv; s.count = 2; return; }
+        if (d13_1 > 0.0f && d13_2 > 0.0f && d123_2 <= 0.0f) { float inv = 1.0f / (d13_1 + d13_2); s.v[0].a = d13_1 * inv; s.v[2].a = d13_2 * inv; s.count = 2; s.v[1] = s.v[2]; return; }
+        if (d12_1 <= 0.0f && d23_2 <= 0.0f) { s.v[1].a = 1.0f; s.count = 1; s.v[0] = s.v[1]; return; }
+        if (d13_1 <= 0.0f && d23_1 <= 0.0f) { s.v[2].a = 1.0f; s.count = 1; s.v[0] = s.v[2]; return; }
+        if (d23_1 > 0.0f && d23_2 > 0.0f && d123_1 <= 0.0f) { float inv = 1.0f / (d23_1 + d23_2); s.v[1].a = d23_1 * inv; s.v[2].a = d23_2 * inv; s.count = 2; s.v[0] = s.v[2]; return; }
+        float inv = 1.0f / (d123_1 + d123_2 + d123_3);
+        s.v[0].a = d123_1 * inv; s.v[1].a = d123_2 * inv; s.v[2].a = d123_3 * inv; s.count = 3;
+    }
+    // b2Distance (GJK), returns distance between the (radius-free) cores
+    __device__ static float gjk(SCache& cache, const DProxy& pA, Xf xA, const DProxy& pB, Xf xB) {
+        Simplex s;
+        s.count = cache.count;
+        for (int i = 0; i < s.count; ++i) {
+            SVert& v = s.v[i];
+            v.iA = cache.iA[i]; v.iB = cache.iB[i];
+            v.wA = mul_xv(xA, pA.v[v.iA]); v.wB = mul_xv(xB, pB.v[v.iB]);
+            v.w = vsub(v.wB, v.wA); v.a = 0.0f;
+        }
+        if (s.count > 1) {
+            float m1 = cache.metric, m2 = s_metric(s);
+            if (m2 < 0.5f * m1 || 2.0f * m1 < m2 || m2 < FLT_EPS) s.count = 0;
+        }
+        if (s.count == 0) {
+            SVert& v = s.v[0];
+            v.iA = 0; v.iB = 0; v.wA = mul_xv(xA, pA.v[0]); v.wB = mul_xv(xB, pB.v[0]);
+            v.w = vsub(v.wB, v.wA); v.a = 1.0f; s.count = 1;
+        }
+        int saveA[3], saveB[3], saveCount;
+        int iter = 0;
+        while (iter < 20) {
+            saveCount = s.count;
+            for (int i = 0; i < saveCount; ++i) { saveA[i] = s.v[i].iA; saveB[i] = s.v[i].iB; }
+            if (s.count == 2) s_solve2(s); else if (s.count == 3) s_solve3(s);
+            if (s.count == 3) break;
+            V2 d;
+            if (s.count == 1) d = vneg(s.v[0].w);
+            else {
+                V2 e12 = vsub(s.v[1].w, s.v[0].w);
+                float sgn = vcross(e12, vneg(s.v[0].w));
+                d = sgn > 0.0f ? vcross_sv(1.0f, e12) : vcross_vs(e12, 1.0f);
+            }
+            if (vlensq(d) < FLT_EPS * FLT_EPS) break;
+            SVert& vt = s.v[s.count];
+            vt.iA = support(pA, mulT_rv(xA.q, vneg(d)));
+            vt.wA = mul_xv(xA, pA.v[vt.iA]);
+            vt.iB = support(pB, mulT_rv(xB.q, d));
+            vt.wB = mul_xv(xB, pB.v[vt.iB]);
+            vt.w = vsub(vt.wB, vt.wA);
+            ++iter;
+            bool dup = false;
+            for (int i = 0; i < saveCount; ++i) if (vt.iA == saveA[i] && vt.iB == saveB[i]) { dup = true; break; }
+            if (dup) break;
+            ++s.count;
+        }
+        V2 pa = v2(0.0f, 0.0f), pb = v2(0.0f, 0.0f);
+        if (s.count == 1) { pa = s.v[0].wA; pb = s.v[0].wB; }
+        else if (s.count == 2) {
+            pa = vadd(vmul(s.v[0].a, s.v[0].wA), vmul(s.v[1].a, s.v[1].wA));
+            pb = vadd(vmul(s.v[0].a, s.v[0].wB), vmul(s.v[1].a, s.v[1].wB));
+        } else if (s.count == 3) {
+            pa = vadd(vadd(vmul(s.v[0].a, s.v[0].wA), vmul(s.v[1].a, s.v[1].wA)), vmul(s.v[2].a, s.v[2].wA));
+            pb = pa;
+        }
+        float dist = vlen(vsub(pa, pb));
+        cache.metric = s_metric(s); cache.count = s.count;
+        for (int i = 0; i < s.count; ++i) { cache.iA[i] = s.v[i].iA; cache.iB[i] = s.v[i].iB; }
+        return dist;
+    }
+    struct SepFn { int type; V2 lp, axis; };
+    __device__ static float sep_eval(const SepFn& f, const DProxy& pA, const DProxy& pB, const SweepV& sA, const SweepV& sB, int iA, int iB, float t) {
+        Xf xA = sweep_xf(sA, t), xB = sweep_xf(sB, t);
+        if (f.type == 0) return vdot(vsub(mul_xv(xB, pB.v[iB]), mul_xv(xA, pA.v[iA])), f.axis);
+        if (f.type == 1) {
+            V2 normal = mul_rv(xA.q, f.axis);
+            V2 pointA = mul_xv(xA, f.lp);
+            return vdot(vsub(mul_xv(xB, pB.v[iB]), pointA), normal);
+        }
+        V2 normal = mul_rv(xB.q, f.axis);
+        V2 pointB = mul_xv(xB, f.lp);
+        return vdot(vsub(mul_xv(xA, pA.v[iA]), pointB), normal);
+    }
+    __device__ static float sep_min(const SepFn& f, const DProxy& pA, const DProxy& pB, const SweepV& sA, const SweepV& sB, int& iA, int& iB, float t) {
+        Xf xA = sweep_xf(sA, t), xB = sweep_xf(sB, t);
+        if (f.type == 0) {
+            iA = support(pA, mulT_rv(xA.q, f.axis)); iB = support(pB, mulT_rv(xB.q, vneg(f.axis)));
+            return vdot(vsub(mul_xv(xB, pB.v[iB]), mul_xv(xA, pA.v[iA])), f.axis);
+        }
+        if (f.type == 1) {
+            V2 normal = mul_rv(xA.q, f.axis);
+            V2 pointA = mul_xv(xA, f.lp);
+            iA = -1; iB = support(pB, mulT_rv(xB.q, vneg(normal)));
+            return vdot(vsub(mul_xv(xB, pB.v[iB]), pointA), normal);
+        }
+        V2 normal = mul_rv(xB.q, f.axis);
+        V2 pointB = mul_xv(xB, f.lp);
+        iB = -1; iA = support(pA, mulT_rv(xA.q, vneg(normal)));
+        return vdot(vsub(mul_xv(xA, pA.v[iA]), pointB), normal);
+    }
+    // b2TimeOfImpact; state 3 == e_touching
+    __device__ static TOIOut time_of_impact(const DProxy& pA, const DProxy& pB, SweepV sA, SweepV sB) {
+        TOIOut out; out.state = 0; out.t = 1.0f;
+        {   // b2Sweep::Normalize
+            float twoPi = 2.0f * B2_PI;
+            float d = twoPi * floorf(sA.a0 / twoPi); sA.a0 -= d; sA.a -= d;
+            d = twoPi * floorf(sB.a0 / twoPi); sB.a0 -= d; sB.a -= d;
+        }
+        const float tMax = 1.0f;
+        float totalRadius = pA.radius + pB.radius;
+        float target = fmax_(LINEAR_SLOP, totalRadius - 3.0f * LINEAR_SLOP);
+        float tolerance = 0.25f * LINEAR_SLOP;
+        float t1 = 0.0f;
+        int iter = 0;
+        SCache cache; cache.count = 0; cache.metric = 0.0f;
+        for (;;) {
+            Xf xA = sweep_xf(sA, t1), xB = sweep_xf(sB, t1);
+            float distance = gjk(cache, pA, xA, pB, xB);
+            if (distance <= 0.0f) { out.state = 2; out.t = 0.0f; break; }
+            if (distance < target + tolerance) { out.state = 3; out.t = t1; break; }
+            SepFn f;
+            if (cache.count == 1) {
+                f.type = 0;
+                f.axis = vsub(mul_xv(xB, pB.v[cache.iB[0]]), mul_xv(xA, pA.v[cache.iA[0]]));
+                vnormalize(f.axis);
+                f.lp = v2(0.0f, 0.0f);
+            } else if (cache.iA[0] == cache.iA[1]) {
+                f.type = 2;
+                V2 b1 = pB.v[cache.iB[0]], b2 = pB.v[cache.iB[1]];
+                f.axis = vcross_vs(vsub(b2, b1), 1.0f);
+                vnormalize(f.axis);
+                V2 normal = mul_rv(xB.q, f.axis);
+                f.lp = vmul(0.5f, vadd(b1, b2));
+                V2 pointB = mul_xv(xB, f.lp);
+                V2 pointA = mul_xv(xA, pA.v[cache.iA[0]]);
+                float s = vdot(vsub(pointA, pointB), normal);
+                if (s < 0.0f) f.axis = vneg(f.axis);
+            } else {
+                f.type = 1;
+                V2 a1 = pA.v[cache.iA[0]], a2 = pA.v[cache.iA[1]];
+                f.axis = vcross_vs(vsub(a2, a1), 1.0f);
+                vnormalize(f.axis);
+                V2 normal = mul_rv(xA.q, f.axis);
+                f.lp = vmul(0.5f, vadd(a1, a2));
+                V2 pointA = mul_xv(xA, f.lp);
+                V2 pointB = mul_xv(xB, pB.v[cache.iB[0]]);
+                float s = vdot(vsub(pointB, pointA), normal);
+                if (s < 0.0f) f.axis = vneg(f.axis);
+            }
+            bool done = false;
+            float t2 = tMax;
+            int pushBackIter = 0;
+            for (;;) {
+                int iA, iB;
+                float s2 = sep_min(f, pA, pB, sA, sB, iA, iB, t2);
+                if (s2 > target + tolerance) { out.state = 4; out.t = tMax; done = true; break; }
+                if (s2 > target - tolerance) { t1 = t2; break; }
+                float s1 = sep_eval(f, pA, pB, sA, sB, iA, iB, t1);
+                if (s1 < target - tolerance) { out.state = 1; out.t = t1; done = true; break; }
+                if (s1 <= target + tolerance) { out.state = 3; out.t = t1; done = true; break; }
+                int rootIter = 0;
+                float a1 = t1, a2 = t2;
+                for (;;) {
+                    float t;
+                    if (rootIter & 1) t = a1 + (target - s1) * (a2 - a1) / (s2 - s1);
+                    else t = 0.5f * (a1 + a2);
+                    ++rootIter;
+                    float s = sep_eval(f, pA, pB, sA, sB, iA, iB, t);
+                    if (fabsf(s - target) < tolerance) { t2 = t; break; }
+                    if (s > target) { a1 = t; s1 = s; } else { a2 = t; s2 = s; }
+                    if (rootIter == 50) break;
+                }
+                ++pushBackIter;
+                if (pushBackIter == MAX_POLY) break;
+            }
+            ++iter;
+            if (done) break;
+            if (iter == 20) { out.state = 1; out.t = t1; break; }
+        }
+        return out;
+    }
+
+    // b2Island::SolveTOI
+    __device__ void island_solve_toi(Isl& is, float dt, int toiA, int toiB, VC* vcs, PC* pcs, const float* salpha0) {
+        for (int i = 0; i < is.nb; ++i) {
+            int b = is.bodies[i];
+            if (is_dyn(b)) { is.pcx[i] = S.cx[b]; is.pcy[i] = S.cy[b]; is.pa[i] = S.a[b]; is.vvx[i] = S.vx[b]; is.vvy[i] = S.vy[b]; is.vw[i] = S.w[b]; }
+            else { V2 c = center(b); is.pcx[i] = c.x; is.pcy[i] = c.y; is.pa[i] = 0.0f; is.vvx[i] = 0.0f; is.vvy[i] = 0.0f; is.vw[i] = 0.0f; }
+        }
+        solver_init(is, vcs, pcs, false, 1.0f);
+        for (int i = 0; i < 20; ++i) if (solver_position(is, pcs, true, toiA, toiB)) break;
+        {
+            int ba = is.bodies[toiA], bb = is.bodies[toiB];
+            if (is_dyn(ba)) { S.c0x[ba] = is.pcx[toiA]; S.c0y[ba] = is.pcy[toiA]; S.a0[ba] = is.pa[toiA]; }
+            if (is_dyn(bb)) { S.c0x[bb] = is.pcx[toiB]; S.c0y[bb] = is.pcy[toiB]; S.a0[bb] = is.pa[toiB]; }
+        }
+        solver_init_velocity(is, vcs, pcs);
+        for (int i = 0; i < 180; ++i) solver_velocity(is, vcs);
+        integrate_positions(is, dt);
+        for (int i = 0; i < is.nb; ++i) {
+            int b = is.bodies[i];
+            if (!is_dyn(b)) continue;
+            S.cx[b] = is.pcx[i]; S.cy[b] = is.pcy[i]; S.a[b] = is.pa[i];
+            S.vx[b] = is.vvx[i]; S.vy[b] = is.vvy[i]; S.w[b] = is.vw[i];
+            sync_transform(b);
+        }
+    }
+
+    // b2World::SolveTOI
+    __device__ void solve_toi(float dt) {
+        float salpha0[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (int b = 0; b < ND; ++b) S.alpha0[b] = 0.0f;
+        for (int c = S.cHead; c != NULLN; c = S.cnext[c]) { S.cflags[c] &= ~(CF_TOI | CF_ISLAND); S.ctoiCount[c] = 0; S.ctoi[c] = 1.0f; }
+        Isl is;
+        VC vcs[MAX_TOI_CONTACTS];
+        PC pcs[MAX_TOI_CONTACTS];
+        bool bflag[NBODY];
+        for (int b = 0; b < NBODY; ++b) bflag[b] = false;
+        for (;;) {
+            int minC = NULLN; float minAlpha = 1.0f;
+            for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
+                if ((S.cflags[c] & CF_ENABLED) == 0) continue;
+                if (S.ctoiCount[c] > MAX_SUBSTEPS) continue;
+                float alpha = 1.0f;
+                if (S.cflags[c] & CF_TOI) {
+                    alpha = S.ctoi[c];
+                } else {
+                    int fa = S.cfa[c], fb = S.cfb[c];
+                    int bA = T.fix_body[fa], bB = T.fix_body[fb];
+                    bool collideA = !is_dyn(bA), collideB = !is_dyn(bB);   // no bullets in these envs
+                    if (!collideA && !collideB) continue;
+                    SweepV sA = sweep(bA, salpha0), sB = sweep(bB, salpha0);
+                    float alpha0 = sA.alpha0;
+                    if (sA.alpha0 < sB.alpha0) { alpha0 = sB.alpha0; sweep_advance(sA, alpha0); sweep_store(bA, sA, salpha0); }
+                    else if (sB.alpha0 < sA.alpha0) { alpha0 = sA.alpha0; sweep_advance(sB, alpha0); sweep_store(bB, sB, salpha0); }
+                    DProxy pA = { T.shape[fa].v, T.shape[fa].count, T.shape[fa].radius };
+                    DProxy pB = { T.shape[fb].v, T.shape[fb].count, T.shape[fb].radius };
+                    TOIOut o = time_of_impact(pA, pB, sA, sB);
+                    if (o.state == 3) alpha = fmin_(alpha0 + (1.0f - alpha0) * o.t, 1.0f);
+                    else alpha = 1.0f;
+                    S.ctoi[c] = alpha;
+                    S.cflags[c] |= CF_TOI;
+                }
+                if (alpha < minAlpha) { minC = c; minAlpha = alpha; }
+            }
+            if (minC == NULLN || 1.0f - 10.0f * FLT_EPS < minAlpha) break;
+            ++S.toiEvents;
+            int fa = S.cfa[minC], fb = S.cfb[minC];
+            int bA = T.fix_body[fa], bB = T.fix_body[fb];
+            SweepV back1 = sweep(bA, salpha0), back2 = sweep(bB, salpha0);
+            body_advance(bA, minAlpha, salpha0);
+            body_advance(bB, minAlpha, salpha0);
+            contact_update(minC);
+            S.cflags[minC] &= ~CF_TOI;
+            ++S.ctoiCount[minC];
+            if ((S.cflags[minC] & CF_ENABLED) == 0 || (S.cflags[minC] & CF_TOUCHING) == 0) {
+                S.cflags[minC] &= ~CF_ENABLED;
+                sweep_store(bA, back1, salpha0); sweep_store(bB, back2, salpha0);
+                if (bA < ND) sync_transform(bA);
+                if (bB < ND) sync_transform(bB);
+                continue;
+            }
+            is.nb = 0; is.nc = 0;
+            island_add_body(is, bA); island_add_body(is, bB);
+            is.contacts[is.nc++] = minC;
+            bflag[bA] = true; bflag[bB] = true;
+            S.cflags[minC] |= CF_ISLAND;
+            int pair[2] = {bA, bB};
+            for (int k = 0; k < 2; ++k) {
+                int body = pair[k];
+                if (!is_dyn(body)) continue;
+                for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
+                    int cA = T.fix_body[S.cfa[c]], cB = T.fix_body[S.cfb[c]];
+                    if (cA != body && cB != body) continue;
+                    if (is.nb == 2 * MAX_TOI_CONTACTS) break;
+                    if (is.nc == MAX_TOI_CONTACTS) break;
+                    if (S.cflags[c] & CF_ISLAND) continue;
+                    int other = cA == body ? cB : cA;
+                    if (is_dyn(other)) continue;   // only static (no bullets/kinematic here)
+                    SweepV backup = sweep(other, salpha0);
+                    if (!bflag[other]) body_advance(other, minAlpha, salpha0);
+                    contact_update(c);
+                    if ((S.cflags[c] & CF_ENABLED) == 0 || (S.cflags[c] & CF_TOUCHING) == 0) {
+                        sweep_store(other, backup, salpha0);
+                        if (other < ND) sync_transform(other);
+                        continue;
+                    }
+                    S.cflags[c] |= CF_ISLAND;
+                    is.contacts[is.nc++] = c;
+                    if (bflag[other]) continue;
+                    bflag[other] = true;
+                    island_add_body(is, other);
+                }
+            }
+            island_solve_toi(is, (1.0f - minAlpha) * dt, is.index[bA], is.index[bB], vcs, pcs, salpha0);
+            for (int i = 0; i < is.nb; ++i) {
+                int body = is.bodies[i];
+                bflag[body] = false;
+                if (!is_dyn(body)) continue;
+                sync_fixtures(body);
+                for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
+                    int cA = T.fix_body[S.cfa[c]], cB = T.fix_body[S.cfb[c]];
+                    if (cA == body || cB == body) S.cflags[c] &= ~(CF_TOI | CF_ISLAND);
+                }
+            }
+            find_new_contacts();
+        }
+    }
+
+    // b2World::Step(1/50, 180, 60)
+    __device__ void world_step() {
+        const float dt = 1.0f / 50;
+        if (S.newFixture) { find_new_contacts(); S.newFixture = 0; }
+        float inv_dt = 1.0f / dt;
+        float dtRatio = S.inv_dt0 * dt;
+        collide();
+        solve(dt, dtRatio);
+        solve_toi(dt);
+        S.inv_dt0 = inv_dt;
+        for (int b = 0; b < ND; ++b) { S.fx[b] = 0.0f; S.fy[b] = 0.0f; S.tq[b] = 0.0f; }
+    }
+};
+
+}  // namespace mrp

@@ -1,0 +1,53 @@
+"""Host-side spawn draws in the reference's order (the reference draws from numpy's
+*global* ``np.random``, not ``self.np_random``).
+
+``reference_draws(env_id, rs)`` returns exactly the float64 values the reference's
+``np.random.uniform(low, high)`` calls produce, in call order:
+
+* v0 / Heavy-v0 (``multi_robot_puzzle_00.py:311-315,366-367``): block x, y, angle, then
+  x, y per agent.
+* v2 / Heavy-v2 (``multi_robot_puzzle_02.py:324,358-359,307-308``): block angle, then x, y
+  per agent, then goal x, y (``_set_random_goal``; SIMPLE=True places the block at the
+  screen centre and fixes agent heading at 3/2*pi).
+* 3-block (build-defined): one angle per block (T, L, I), agents, goal.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+# v0 constants (multi_robot_puzzle_00.py:38-43)
+_V0_SCALE, _V0_W, _V0_H, _V0_BORDER = 30.0, 640, 480, 1
+# v2 constants (multi_robot_puzzle_02.py:39-44, 305)
+_V2_SCALE, _V2_W, _V2_H, _V2_BORDER, _V2_GOAL_BORDER = 140.0 * 4, 1440, 810, 0.3, 0.4
+
+N_AGENTS = {0: 2, 1: 5, 2: 2, 3: 2, 4: 2}
+N_BLOCKS = {0: 1, 1: 1, 2: 1, 3: 1, 4: 3}
+
+
+def draw_bounds(env_id: int):
+    """(low, high) of every uniform draw of one reset, in call order."""
+    b = []
+    if env_id in (0, 1):
+        xr = (_V0_BORDER, _V0_W / _V0_SCALE - _V0_BORDER)
+        yr = (_V0_BORDER, _V0_H / _V0_SCALE - _V0_BORDER)
+        b += [xr, yr, (0, 2 * np.pi)]
+        b += [xr, yr] * N_AGENTS[env_id]
+    else:
+        b += [(0, 2 * np.pi)] * N_BLOCKS[env_id]
+        xr = (_V2_BORDER, _V2_W / _V2_SCALE / 3 - _V2_BORDER)
+        yr = (_V2_BORDER, _V2_H / _V2_SCALE - _V2_BORDER)
+        b += [xr, yr] * N_AGENTS[env_id]
+        b += [(_V2_W / _V2_SCALE * 2 / 3 + _V2_GOAL_BORDER, _V2_W / _V2_SCALE - _V2_GOAL_BORDER),
+              (_V2_GOAL_BORDER, _V2_H / _V2_SCALE - _V2_GOAL_BORDER)]
+    return b
+
+
+def reference_draws(env_id: int, rs=None) -> np.ndarray:
+    """Draw one reset's spawn values from ``rs`` (a RandomState; default: global np.random)."""
+    rs = np.random if rs is None else rs
+    return np.array([rs.uniform(lo, hi) for lo, hi in draw_bounds(env_id)], dtype=np.float64)
+
+
+def sample_action(act_dim: int, rs) -> np.ndarray:
+    """gym 0.21 ``Box.sample()`` for a bounded [-1, 1] box: uniform(low, high).astype(float32)."""
+    return rs.uniform(low=-np.ones(act_dim), high=np.ones(act_dim), size=(act_dim,)).astype(np.float32)

@@ -1,0 +1,125 @@
+/*
+ * mrp.h -- C ABI of the MI355X-native MultiRobotPuzzle step library (libmrp.so).
+ *
+ * Drop-in boundary for the gym_puzzles hot path.  In the reference the per-step work is
+ * Python driving pybox2d object-by-object (~20 SWIG crossings per agent per step plus
+ * C++->Python contact callbacks); here one call advances N independent worlds ("lanes")
+ * on one GPU.  Each entry point names the reference interface it replaces.
+ *
+ * Conventions
+ *   - Plain C types only; all arrays are row-major [n_lanes][dim].
+ *   - Functions return 0 on success, a negative MRP_E* code on failure; mrp_last_error()
+ *     gives the message (per context, or the last create failure when ctx == NULL).
+ *   - "_device" variants take device pointers (hipMalloc / torch.cuda tensors) and are
+ *     asynchronous on the context's stream; the plain variants take host pointers and
+ *     synchronize.
+ *   - Not re-entrant per context; one context per (device, stream, thread).
+ *
+ * env_id:  0 MultiRobotPuzzle-v0       (gym_puzzles/__init__.py:3-8,  multi_robot_puzzle_00.py:142)
+ *          1 MultiRobotPuzzleHeavy-v0  (gym_puzzles/__init__.py:10-15, multi_robot_puzzle_00.py:606)
+ *          2 MultiRobotPuzzle-v2       (gym_puzzles/__init__.py:17-22, multi_robot_puzzle_02.py:126)
+ *          3 MultiRobotPuzzleHeavy-v2  (gym_puzzles/__init__.py:24-29, multi_robot_puzzle_02.py:711)
+ *          4 MultiRobotPuzzleHeavy-v2 with the build-defined 3-block square
+ */
+#ifndef MRP_H
+#define MRP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MRP_OK 0
+#define MRP_E_ARG (-1)     /* bad argument (env id, lane count, null pointer) */
+#define MRP_E_HIP (-2)     /* HIP runtime error (no device, launch failure, OOM) */
+#define MRP_E_STATE (-3)   /* call order violation (e.g. step before reset) */
+
+/* lane status codes written by mrp_step (the reference's done_status strings) */
+#define MRP_STATUS_RUNNING 0
+#define MRP_STATUS_PUZZLE_COMPLETE 1   /* multi_robot_puzzle_00.py:515-519, _02.py:575-582 */
+#define MRP_STATUS_AGENT_OOB 2         /* multi_robot_puzzle_02.py:552-556 */
+#define MRP_STATUS_BLOCK_OOB 3         /* multi_robot_puzzle_02.py:558-562 */
+
+typedef struct mrp_ctx mrp_ctx;
+
+/* Static dimensions of an env id: observation_space / action_space shapes
+ * (multi_robot_puzzle_00.py:186-207, _02.py:174-195), number of spawn draws per reset,
+ * agents, blocks and the TimeLimit max_episode_steps (gym_puzzles/__init__.py:6-27). */
+int mrp_env_dims(int env_id, int* obs_dim, int* act_dim, int* n_draws, int* n_agents, int* n_blocks,
+                 int* max_episode_steps);
+
+/* Create n_lanes worlds on HIP device `device`.  Replaces gym.make(id) ->
+ * MultiRobotPuzzle.__init__ (multi_robot_puzzle_00.py:152-209): one Box2D.b2World per lane
+ * (gravity 0, no sleep).  `seed` keys the on-device counter RNG (device resets, synthetic
+ * actions); `lane_offset` is the global index of lane 0 (multi-GPU sharding keeps per-lane
+ * streams identical for any GPU count).  Worlds are empty until mrp_reset. */
+int mrp_create(int env_id, int n_lanes, int device, uint64_t seed, uint64_t lane_offset, mrp_ctx** out);
+void mrp_destroy(mrp_ctx* ctx);
+const char* mrp_last_error(const mrp_ctx* ctx);
+int mrp_n_lanes(const mrp_ctx* ctx);
+int mrp_env_id(const mrp_ctx* ctx);
+
+/* Use this hipStream_t (NULL = the context's own stream) for all subsequent work. */
+int mrp_set_stream(mrp_ctx* ctx, void* hip_stream);
+int mrp_synchronize(mrp_ctx* ctx);
+
+/* set_reward_params (multi_robot_puzzle_00.py:231-239, _02.py:216-225). */
+int mrp_set_reward_params(mrp_ctx* ctx, double agent_delta, double agent_distance, double block_delta,
+                          double block_distance, double puzzle_comp, double out_of_bounds, double blk_out_of_bounds);
+/* update_params(timestep, decay) (multi_robot_puzzle_00.py:241-243, _02.py:227-230). */
+int mrp_update_params(mrp_ctx* ctx, double timestep, double decay);
+/* update_goal(epoch, nb_epochs) (multi_robot_puzzle_00.py:245-246, _02.py:232-233). */
+int mrp_update_goal(mrp_ctx* ctx, double epoch, double nb_epochs);
+
+/* reset() (multi_robot_puzzle_00.py:392-411, _02.py:421-442) for the lanes whose
+ * lane_mask byte is nonzero (NULL = all): destroy + rebuild the bodies in the reference's
+ * order, then the reference's extra physics step with a random action.
+ *   draws   [n_lanes][n_draws] float64: the np.random.uniform(...) values the reference
+ *           draws (gym_puzzles_amd/spawn.py); NULL = device counter RNG.
+ *   actions [n_lanes][act_dim] float32: the reset step's action_space.sample(); NULL = RNG.
+ *   obs     [n_lanes][obs_dim] float32 out (rows of unmasked lanes are left untouched). */
+int mrp_reset(mrp_ctx* ctx, const uint8_t* lane_mask, const double* draws, const float* actions, float* obs);
+int mrp_reset_device(mrp_ctx* ctx, const uint8_t* d_lane_mask, const double* d_draws, const float* d_actions,
+                     float* d_obs);
+
+/* step(action) (multi_robot_puzzle_00.py:413-521, _02.py:444-584) under gym's TimeLimit
+ * wrapper, for all lanes:
+ *   actions  [n_lanes][act_dim] float32 (NULL = device RNG uniform[-1,1), keyed by lane/step)
+ *   obs      [n_lanes][obs_dim] float32 out (the reference returns float64; values are
+ *            float32(reference value))
+ *   reward   [n_lanes] float32 out, done/truncated [n_lanes] uint8 out
+ *            (truncated = TimeLimit.truncated), status [n_lanes] uint8 out (MRP_STATUS_*),
+ *   terminal_obs [n_lanes][obs_dim] float32 out or NULL: when auto-reset is on, done lanes
+ *            are reset on device (RNG spawns) and obs holds the new episode's first
+ *            observation while terminal_obs holds the last one (SB3 VecEnv semantics).
+ * Any output pointer except obs may be NULL. */
+int mrp_step(mrp_ctx* ctx, const float* actions, float* obs, float* reward, uint8_t* done, uint8_t* truncated,
+             uint8_t* status, float* terminal_obs);
+int mrp_step_device(mrp_ctx* ctx, const float* d_actions, float* d_obs, float* d_reward, uint8_t* d_done,
+                    uint8_t* d_truncated, uint8_t* d_status, float* d_terminal_obs);
+int mrp_set_auto_reset(mrp_ctx* ctx, int enabled);
+/* TimeLimit max_episode_steps applied inside mrp_step (default: the registered value of
+ * gym_puzzles/__init__.py:6-27); 0 disables it (when an outer gym.wrappers.TimeLimit is used). */
+int mrp_set_time_limit(mrp_ctx* ctx, int max_episode_steps);
+
+/* Introspection (tests, checkpointing).  Dynamic bodies in creation order (blocks, agents),
+ * 6 floats each: worldCenter.x, worldCenter.y, angle, linearVelocity.x, .y, angularVelocity. */
+int mrp_get_bodies(mrp_ctx* ctx, float* out /* [n_lanes][6*(n_blocks+n_agents)] */);
+/* per lane: goal_contact flags [n_agents] then blks_in_place -> int32 [n_lanes][n_agents+1] */
+int mrp_get_flags(mrp_ctx* ctx, int32_t* out);
+/* summed over lanes: TOI events and position-solver iterations (diagnostics) */
+int mrp_counters(mrp_ctx* ctx, int64_t* toi_events, int64_t* pos_iters);
+/* Raw per-lane state (checkpoint / resume): mrp_state_words() 32-bit words per lane. */
+int mrp_state_words(int env_id);
+int mrp_get_state(mrp_ctx* ctx, uint32_t* out /* [n_lanes][state_words] */);
+int mrp_set_state(mrp_ctx* ctx, const uint32_t* in);
+
+/* Device self-test of the glibc-faithful sinf/cosf used by every b2Rot::Set on the GPU:
+ * evaluates them on device `device` for n host inputs (host output arrays). */
+int mrp_selftest_sincos(int device, const float* x, float* sin_out, float* cos_out, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,57 @@
+/*
+ * mrp_oracle.h -- TEST INFRASTRUCTURE ONLY (parity oracle; never linked into the product).
+ *
+ * CPU restatement of one MultiRobotPuzzle environment (one "lane"): the gym_puzzles
+ * env logic of gym_puzzles/envs/multi_robot_puzzle_00.py (v0, Heavy-v0) and
+ * multi_robot_puzzle_02.py (v2, Heavy-v2), driving the Box2D restatement in
+ * b2_oracle.c.  Python float64 semantics (numpy 1.x scalar promotion, CPython float
+ * pow/mod) are reproduced for the env-level arithmetic; the engine runs in float32.
+ *
+ * Parity against pybox2d is UNPINNED (no pybox2d / gym in this image and no reference
+ * fixture pins a step result; SURVEY.md sections 4 and 8c).
+ */
+#ifndef MRP_ORACLE_H
+#define MRP_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct OrEnv OrEnv;
+
+/* env ids (same numbering as include/mrp.h) */
+int or_obs_dim(int env_id);
+int or_act_dim(int env_id);
+int or_n_draws(int env_id);
+int or_n_agents(int env_id);
+int or_n_blocks(int env_id);
+int or_max_episode_steps(int env_id);
+
+OrEnv* or_create(int env_id);
+void or_destroy(OrEnv* e);
+/* reset(): draws are the values np.random.uniform(...) returns, in reference draw order;
+ * action is the float32 action_space.sample() the reference feeds to its reset step. */
+void or_reset(OrEnv* e, const double* draws, const float* reset_action, double* obs_out);
+/* step(): returns env done (not TimeLimit) and terminal kind
+ * (0 none, 1 puzzle complete, 2 agent out of bounds, 3 block out of bounds). */
+void or_step(OrEnv* e, const float* action, double* obs_out, double* reward, int* done, int* kind);
+void or_set_shaped(OrEnv* e, double bounds_penalty, double blk_bounds_penalty, double puzzle_reward);
+/* dynamic body state in creation order (blocks, then agents): c.x c.y a v.x v.y w */
+int or_get_bodies(const OrEnv* e, float* out);
+void or_get_flags(const OrEnv* e, int* goal_contact, int* blks_in_place);
+int or_contact_count(const OrEnv* e);
+void or_counters(const OrEnv* e, long* toi_events, long* pos_iters);
+/* proxy ids of all fixtures in creation order (blocks, agents, walls) */
+int or_proxy_ids(const OrEnv* e, int* out);
+
+/* glibc-faithful math exported for tests */
+float or_sinf(float x);
+float or_cosf(float x);
+
+/* counter-based RNG shared with the device path (integer SplitMix64 mix) */
+double or_rng_u01(uint64_t seed, uint64_t lane, uint64_t stream, uint64_t counter);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,144 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes front end of the CPU parity oracle.
+
+Loads ``oracle/build/libmrp_oracle.so`` (plain-C restatement of the gym_puzzles step path
+and the Box2D v2.3 subset it calls; see ``oracle/b2_oracle.h``).  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import this module;
+the product (``gym_puzzles_amd``) never does.
+
+Parity of this oracle against pybox2d is UNPINNED: the reference's own tests pin no step
+result and box2d-py is not importable in this image (SURVEY.md sections 4, 8c).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libmrp_oracle.so")
+_lib = None
+
+ENV_IDS = {
+    "MultiRobotPuzzle-v0": 0,
+    "MultiRobotPuzzleHeavy-v0": 1,
+    "MultiRobotPuzzle-v2": 2,
+    "MultiRobotPuzzleHeavy-v2": 3,
+    "MultiRobotPuzzleHeavy-v2-3block": 4,
+}
+
+
+def build() -> str:
+    """Compile the oracle with its committed Makefile (gcc, -ffp-contract=off)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        c_int, c_float, c_double = ctypes.c_int, ctypes.c_float, ctypes.c_double
+        P = ctypes.c_void_p
+        for name in ("or_obs_dim", "or_act_dim", "or_n_draws", "or_n_agents", "or_n_blocks", "or_max_episode_steps"):
+            getattr(L, name).argtypes = [c_int]
+            getattr(L, name).restype = c_int
+        L.or_create.argtypes = [c_int]
+        L.or_create.restype = P
+        L.or_destroy.argtypes = [P]
+        L.or_reset.argtypes = [P, P, P, P]
+        L.or_step.argtypes = [P, P, P, P, P, P]
+        L.or_set_shaped.argtypes = [P, c_double, c_double, c_double]
+        L.or_get_bodies.argtypes = [P, P]
+        L.or_get_bodies.restype = c_int
+        L.or_get_flags.argtypes = [P, P, P]
+        L.or_contact_count.argtypes = [P]
+        L.or_contact_count.restype = c_int
+        L.or_counters.argtypes = [P, P, P]
+        L.or_proxy_ids.argtypes = [P, P]
+        L.or_proxy_ids.restype = c_int
+        L.or_sinf.argtypes = [c_float]
+        L.or_sinf.restype = c_float
+        L.or_cosf.argtypes = [c_float]
+        L.or_cosf.restype = c_float
+        L.or_rng_u01.argtypes = [ctypes.c_uint64] * 4
+        L.or_rng_u01.restype = c_double
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class OracleEnv:
+    """One lane of the CPU oracle (one b2World that persists across resets, like the reference)."""
+
+    def __init__(self, env_id: int):
+        L = lib()
+        self.env_id = env_id
+        self.obs_dim = L.or_obs_dim(env_id)
+        self.act_dim = L.or_act_dim(env_id)
+        self.n_draws = L.or_n_draws(env_id)
+        self.n_agents = L.or_n_agents(env_id)
+        self.n_blocks = L.or_n_blocks(env_id)
+        self.max_episode_steps = L.or_max_episode_steps(env_id)
+        self._h = L.or_create(env_id)
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.or_destroy(self._h)
+            self._h = None
+
+    def reset(self, draws, action) -> np.ndarray:
+        d = np.ascontiguousarray(draws, dtype=np.float64)
+        a = np.ascontiguousarray(action, dtype=np.float32)
+        assert d.size == self.n_draws and a.size == self.act_dim
+        obs = np.zeros(self.obs_dim, np.float64)
+        lib().or_reset(self._h, _ptr(d), _ptr(a), _ptr(obs))
+        return obs
+
+    def step(self, action):
+        a = np.ascontiguousarray(action, dtype=np.float32)
+        assert a.size == self.act_dim
+        obs = np.zeros(self.obs_dim, np.float64)
+        rew = np.zeros(1, np.float64)
+        done = np.zeros(1, np.int32)
+        kind = np.zeros(1, np.int32)
+        lib().or_step(self._h, _ptr(a), _ptr(obs), _ptr(rew), _ptr(done), _ptr(kind))
+        return obs, float(rew[0]), bool(done[0]), int(kind[0])
+
+    def set_shaped(self, bounds, blk_bounds, puzzle):
+        lib().or_set_shaped(self._h, bounds, blk_bounds, puzzle)
+
+    def bodies(self) -> np.ndarray:
+        out = np.zeros(6 * (self.n_agents + self.n_blocks), np.float32)
+        lib().or_get_bodies(self._h, _ptr(out))
+        return out
+
+    def flags(self):
+        gc = np.zeros(self.n_agents, np.int32)
+        bip = np.zeros(1, np.int32)
+        lib().or_get_flags(self._h, _ptr(gc), _ptr(bip))
+        return gc, int(bip[0])
+
+    def contact_count(self) -> int:
+        return lib().or_contact_count(self._h)
+
+    def counters(self):
+        a = np.zeros(1, np.int64)
+        b = np.zeros(1, np.int64)
+        lib().or_counters(self._h, _ptr(a), _ptr(b))
+        return int(a[0]), int(b[0])
+
+    def proxy_ids(self) -> np.ndarray:
+        out = np.zeros(64, np.int32)
+        n = lib().or_proxy_ids(self._h, _ptr(out))
+        return out[:n].copy()
+
+
+def rng_u01(seed: int, lane: int, stream: int, counter: int) -> float:
+    return lib().or_rng_u01(seed, lane, stream, counter)
