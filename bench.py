@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/sec of the MI355X-native MultiRobotPuzzle step (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): MultiRobotPuzzle-v0, 4096 lanes (independent worlds) per
+GPU, synthetic random actions generated on device (counter RNG keyed by global lane and step),
+gym TimeLimit + done -> on-device auto-reset inside the timed loop (as SB3's VecEnv would).
+A "step" is one k_step launch advancing every lane of every rank by one env step.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--env ID] [--lanes L]
+
+For N > 1 launch one process per GPU (torch.distributed.run); lanes shard contiguously
+(rank r owns global lanes [r*L, (r+1)*L)), per-lane trajectories are independent of N, and
+each step ends with one gather of (obs, reward, done) to rank 0 (the policy rank).
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+ENV_NAMES = {0: "MultiRobotPuzzle-v0", 1: "MultiRobotPuzzleHeavy-v0", 2: "MultiRobotPuzzle-v2",
+             3: "MultiRobotPuzzleHeavy-v2", 4: "MultiRobotPuzzleHeavy-v2-3block"}
+# Algorithmic HBM bytes per env-step: mutable per-lane state read+written
+# once per step plus I/O; shared geometry/mass tables excluded.
+ALGO_BYTES = {0: 1657, 1: 3547, 2: 3613, 3: 3613, 4: 6085}
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
+
+
+def cpu_baseline(env_id: int, lanes: int = 256, steps: int = 1500) -> dict:
+    """Time the CPU oracle (plain-C restatement, one core) on a bounded sample."""
+    from gym_puzzles_amd.spawn import reference_draws
+    from oracle.oracle import OracleEnv, rng_u01  # noqa: F401  (test infrastructure: baseline leg only)
+    rs = np.random.RandomState(17)
+    envs = [OracleEnv(env_id) for _ in range(lanes)]
+    act_dim = envs[0].act_dim
+    for l, e in enumerate(envs):
+        e.reset(reference_draws(env_id, np.random.RandomState(17 + l)), rs.uniform(-1, 1, act_dim).astype(np.float32))
+    acts = rs.uniform(-1, 1, size=(steps, lanes, act_dim)).astype(np.float32)
+    t0 = time.perf_counter()
+    n = 0
+    for t in range(steps):
+        for l, e in enumerate(envs):
+            _, _, done, _ = e.step(acts[t, l])
+            n += 1
+            if done:
+                e.reset(reference_draws(env_id, np.random.RandomState(10_000 + n)), acts[t, l])
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{ENV_NAMES[env_id]}: {lanes} lanes x {steps} steps of the C oracle (oracle/), 1 host core, "
+                      f"random actions, {dt:.1f} s"}
+
+
+def load_traffic(env_id: int, lanes: int):
+    """HBM bytes per k_step launch from the committed rocprofv3 PMC pass (profiles/), or None."""
+    path = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get(str(env_id))
+        if e and int(e.get("lanes", -1)) == lanes:
+            return float(e["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--env", type=int, default=0)
+    ap.add_argument("--lanes", type=int, default=4096, help="lanes (worlds) per GPU")
+    ap.add_argument("--seed", type=int, default=17)
+    ap.add_argument("--no-gather", action="store_true", help="N>1: skip the per-step gather to rank 0")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from gym_puzzles_amd import Batch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("for --gpus > 1 launch with torch.distributed.run --nproc-per-node N")
+    distributed = world > 1
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU (libmrp has no CPU fallback)")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if distributed:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    L = args.lanes
+    b = Batch(args.env, L, device=local_rank, seed=args.seed, lane_offset=rank * L)
+    # a dedicated (non-NULL) stream shared by the library and torch, so the HIP events that
+    # time k_step are recorded on the stream the kernel runs on
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    b.set_stream(stream.cuda_stream)
+    b.set_auto_reset(True)
+    O = b.obs_dim
+    obs = torch.zeros((L, O), dtype=torch.float32, device=dev)
+    rew = torch.zeros(L, dtype=torch.float32, device=dev)
+    done = torch.zeros(L, dtype=torch.uint8, device=dev)
+    trunc = torch.zeros(L, dtype=torch.uint8, device=dev)
+    # one contiguous buffer per rank for the gather: [obs | reward | done] as float32
+    packed = torch.zeros((L, O + 2), dtype=torch.float32, device=dev)
+    gathered = [torch.zeros_like(packed) for _ in range(world)] if (distributed and rank == 0) else None
+
+    b.reset()   # device-RNG spawns for every lane (seeded by global lane id)
+
+    def one_step():
+        b.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), trunc.data_ptr())
+        if distributed and not args.no_gather:
+            packed[:, :O].copy_(obs)
+            packed[:, O].copy_(rew)
+            packed[:, O + 1].copy_(done)
+            dist.gather(packed, gathered, dst=0)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize(dev)
+
+    K = args.steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(K):
+        ev[k][0].record(stream)
+        b.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), trunc.data_ptr())
+        ev[k][1].record(stream)
+        if distributed and not args.no_gather:
+            packed[:, :O].copy_(obs)
+            packed[:, O].copy_(rew)
+            packed[:, O + 1].copy_(done)
+            dist.gather(packed, gathered, dst=0)
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    if distributed:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    toi, pos = b.counters() if rank == 0 else (0, 0)
+    if rank == 0:
+        total_steps = world * L * K
+        value = total_steps / elapsed
+        algo_bytes = ALGO_BYTES[args.env] * L
+        achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+        traffic = load_traffic(args.env, L)
+        line = {
+            "metric": "env-steps/sec (whole node) at N envs/GPU",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32 (engine) + f64 (env arithmetic)",
+            "data": "synthetic: device-RNG random actions, device-RNG spawns (reference draw ranges)",
+            "config": {"workload": f"{ENV_NAMES[args.env]}, {L} lanes/GPU, random actions, auto-reset",
+                       "lanes_per_gpu": L, "global_lanes": world * L,
+                       "parallelism": f"lane-sharded x{world}" + ("" if world == 1 or args.no_gather else " + gather to rank 0/step")},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic,
+                         "kernel": "k_step", "kernel_ms": kern_ms,
+                         "algorithmic_bytes_per_launch": algo_bytes,
+                         "note": "latency/VALU-bound sequential-impulse solver; HBM fraction reported as the north star asks"},
+            "diagnostics": {"toi_events_total": toi, "position_iterations_total": pos},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.env)
+        print(json.dumps(line), flush=True)
+    b.close()
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -27,10 +27,10 @@ constexpr double TWO_PI = 6.283185307179586;
 template <int ENV> struct Env : World<ENV> {
     using W = World<ENV>;
     using D = Dims<ENV>;
-    using W::S; using W::T; using W::P;
+    using W::S; using W::T; using W::P; using W::sh; using W::tid;
     static constexpr int NA = D::NA, NB = D::NB, ND = W::ND, NF = D::NF;
 
-    __device__ Env(typename W::LS& s, const EnvTables& t, const EnvParams& p) : W(s, t, p) {}
+    __device__ Env(typename W::SH& s, const EnvTables& t, const EnvParams& p, int thread) : W(s, t, p, thread) {}
 
     __device__ void init_empty_world() {   // fresh b2World (Box2D.b2World(gravity=(0,0), doSleep=False))
         for (int i = 0; i < TREE_N; ++i) { S.tpar[i] = i + 1 < TREE_N ? i + 1 : NULLN; S.th[i] = -1; S.tud[i] = -1; S.tc1[i] = NULLN; S.tc2[i] = NULLN; }
@@ -281,22 +281,31 @@ template <int ENV> struct Env : World<ENV> {
         reward_out = reward; done_out = done; kind_out = kind;
     }
 
-    __device__ void env_step(const float* act, float* obs, double& reward, int& done, int& kind) {
-        apply_actions(act);
-        this->world_step();
-        double prevA[NA], prevB[NB];
-        for (int i = 0; i < NA; ++i) prevA[i] = S.agent_dist[i];
-        for (int b = 0; b < NB; ++b) prevB[b] = S.block_distance[b];
-        calc_distances();
-        obs_reward(prevA, prevB, obs, reward, done, kind);
+    // one env step (cooperative: every thread of the wave calls it); reads sh.act, writes
+    // sh.obs / sh.reward / sh.done / sh.kind
+    __device__ void env_step_coop() {
+        if (tid == 0) apply_actions(sh.act);
+        __syncthreads();
+        this->world_step_coop();
+        if (tid == 0) {
+            double prevA[NA], prevB[NB];
+            for (int i = 0; i < NA; ++i) prevA[i] = S.agent_dist[i];
+            for (int b = 0; b < NB; ++b) prevB[b] = S.block_distance[b];
+            calc_distances();
+            obs_reward(prevA, prevB, sh.obs, sh.reward, sh.done, sh.kind);
+        }
+        __syncthreads();
     }
 
-    __device__ void env_reset(const double* draws, const float* act, float* obs) {
-        destroy_bodies();
-        create_bodies(draws);
-        calc_distances();
-        double r; int d, k;
-        env_step(act, obs, r, d, k);
+    // reset(): destroy + rebuild from sh.draws, then the reference's step with sh.act
+    __device__ void env_reset_coop() {
+        if (tid == 0) {
+            destroy_bodies();
+            create_bodies(sh.draws);
+            calc_distances();
+        }
+        __syncthreads();
+        env_step_coop();
     }
 };
 

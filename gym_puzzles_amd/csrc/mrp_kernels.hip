@@ -1,11 +1,13 @@
 // mrp_kernels.hip -- gfx950 kernels and the C ABI (include/mrp.h) of libmrp.so.
 //
-// Round-1 execution model: one GPU thread owns one world ("lane"); a 64-thread block is one
-// wave of 64 worlds.  The persistent lane state lives in HBM structure-of-arrays across lanes
-// (word w of lane l at state[w * n_lanes + l]) so each of the wave's state loads/stores is a
-// single coalesced 256-B transaction; the step itself runs on a private copy.  There is no
-// dense contraction anywhere in this path, so no MFMA: the work is scalar fp32 VALU with
-// data-dependent control flow (contacts, TOI), plus fp64 for the env-level arithmetic.
+// Execution model: one wavefront (64 threads, one workgroup) owns one world ("lane").  The
+// lane's persistent state is contiguous in HBM (lane-major, so the wave moves it with
+// coalesced 256-B loads/stores) and lives in LDS for the whole step; order-sensitive Box2D
+// work (solver iterations, tree updates, contact-list edits, events) runs on thread 0, while
+// the data-parallel phases (SAT narrow phase of every contact, broad-phase pair tests, TOI of
+// every candidate contact, state/obs I/O) are spread over the 64 threads.  There is no dense
+// contraction in this path, so no MFMA: the work is fp32 VALU with data-dependent control
+// flow, plus fp64 for the env-level arithmetic.
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -32,63 +34,71 @@ constexpr int BLOCK = 64;   // one wave per block: lanes of a block never wait o
 typedef uint32_t __attribute__((__may_alias__)) word_t;
 
 template <int ENV>
-__device__ __forceinline__ void load_state(LaneState<ENV>& S, const uint32_t* __restrict__ g, int lane, int nl) {
+__device__ __forceinline__ void load_state(LaneState<ENV>& S, const uint32_t* __restrict__ g, int lane, int tid) {
     word_t* w = reinterpret_cast<word_t*>(&S);
     constexpr int NW = lane_words<ENV>();
-    for (int i = 0; i < NW; ++i) w[i] = g[(size_t)i * nl + lane];
+    const uint32_t* src = g + (size_t)lane * NW;
+    for (int i = tid; i < NW; i += BLOCK) w[i] = src[i];
 }
 template <int ENV>
-__device__ __forceinline__ void store_state(const LaneState<ENV>& S, uint32_t* __restrict__ g, int lane, int nl) {
+__device__ __forceinline__ void store_state(const LaneState<ENV>& S, uint32_t* __restrict__ g, int lane, int tid) {
     const word_t* w = reinterpret_cast<const word_t*>(&S);
     constexpr int NW = lane_words<ENV>();
-    for (int i = 0; i < NW; ++i) g[(size_t)i * nl + lane] = w[i];
+    uint32_t* dst = g + (size_t)lane * NW;
+    for (int i = tid; i < NW; i += BLOCK) dst[i] = w[i];
 }
 
 template <int ENV>
 __global__ __launch_bounds__(BLOCK) void k_init(uint32_t* state, int nl) {
-    int lane = blockIdx.x * BLOCK + threadIdx.x;
+    __shared__ Shared<ENV> sh;
+    const int lane = blockIdx.x, tid = threadIdx.x;
     if (lane >= nl) return;
-    LaneState<ENV> S;
-    memset(&S, 0, sizeof(S));
-    EnvParams P;
-    memset(&P, 0, sizeof(P));
-    Env<ENV> e(S, g_tables[ENV], P);
-    e.init_empty_world();
-    store_state<ENV>(S, state, lane, nl);
+    word_t* w = reinterpret_cast<word_t*>(&sh.S);
+    for (int i = tid; i < lane_words<ENV>(); i += BLOCK) w[i] = 0;
+    __syncthreads();
+    if (tid == 0) {
+        EnvParams P;
+        memset(&P, 0, sizeof(P));
+        Env<ENV> e(sh, g_tables[ENV], P, 0);
+        e.init_empty_world();
+    }
+    __syncthreads();
+    store_state<ENV>(sh.S, state, lane, tid);
 }
 
+// stage one reset's draws/action into LDS: host-provided rows or the counter RNG
 template <int ENV>
-__device__ void lane_reset(Env<ENV>& e, LaneState<ENV>& S, const double* draws, const float* actions, float* obs_row,
-                           int lane, uint64_t seed, uint64_t glane) {
+__device__ void stage_reset_inputs(Shared<ENV>& sh, const double* draws, const float* actions, int lane, int tid,
+                                   uint64_t seed, uint64_t glane) {
     using D = Dims<ENV>;
     const EnvTables& T = g_tables[ENV];
-    double d[D::NDRAW];
-    float a[D::ACT];
-    uint64_t ctr = (uint64_t)(uint32_t)S.episode * 64u;
-    for (int k = 0; k < D::NDRAW; ++k)
-        d[k] = draws ? draws[(size_t)lane * D::NDRAW + k]
-                     : T.draw_lo[k] + (T.draw_hi[k] - T.draw_lo[k]) * rng_u01(seed, glane, 1, ctr + k);
-    for (int j = 0; j < D::ACT; ++j)
-        a[j] = actions ? actions[(size_t)lane * D::ACT + j] : (float)(-1.0 + 2.0 * rng_u01(seed, glane, 2, ctr + j));
-    S.episode += 1;
-    S.elapsed = 0;
-    float o[D::OBS];
-    e.env_reset(d, a, o);
-    for (int k = 0; k < D::OBS; ++k) obs_row[k] = o[k];
+    const uint64_t ctr = (uint64_t)(uint32_t)sh.S.episode * 64u;
+    if (tid < D::NDRAW)
+        sh.draws[tid] = draws ? draws[(size_t)lane * D::NDRAW + tid]
+                              : T.draw_lo[tid] + (T.draw_hi[tid] - T.draw_lo[tid]) * rng_u01(seed, glane, 1, ctr + tid);
+    if (tid < D::ACT)
+        sh.act[tid] = actions ? actions[(size_t)lane * D::ACT + tid] : (float)(-1.0 + 2.0 * rng_u01(seed, glane, 2, ctr + tid));
+    __syncthreads();
+    if (tid == 0) { sh.S.episode += 1; sh.S.elapsed = 0; }
+    __syncthreads();
 }
 
 template <int ENV>
 __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* state, int nl, const uint8_t* mask, const double* draws,
                                                  const float* actions, float* obs, EnvParams P, uint64_t seed,
                                                  uint64_t lane_offset) {
-    int lane = blockIdx.x * BLOCK + threadIdx.x;
+    using D = Dims<ENV>;
+    __shared__ Shared<ENV> sh;
+    const int lane = blockIdx.x, tid = threadIdx.x;
     if (lane >= nl) return;
     if (mask && !mask[lane]) return;
-    LaneState<ENV> S;
-    load_state<ENV>(S, state, lane, nl);
-    Env<ENV> e(S, g_tables[ENV], P);
-    lane_reset<ENV>(e, S, draws, actions, obs + (size_t)lane * Dims<ENV>::OBS, lane, seed, lane_offset + lane);
-    store_state<ENV>(S, state, lane, nl);
+    load_state<ENV>(sh.S, state, lane, tid);
+    __syncthreads();
+    stage_reset_inputs<ENV>(sh, draws, actions, lane, tid, seed, lane_offset + lane);
+    Env<ENV> e(sh, g_tables[ENV], P, tid);
+    e.env_reset_coop();
+    for (int k = tid; k < D::OBS; k += BLOCK) obs[(size_t)lane * D::OBS + k] = sh.obs[k];
+    store_state<ENV>(sh.S, state, lane, tid);
 }
 
 template <int ENV>
@@ -97,33 +107,40 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* state, int nl, const f
                                                 EnvParams P, uint64_t seed, uint64_t lane_offset, int auto_reset,
                                                 int max_steps) {
     using D = Dims<ENV>;
-    int lane = blockIdx.x * BLOCK + threadIdx.x;
+    __shared__ Shared<ENV> sh;
+    __shared__ int s_fin;
+    const int lane = blockIdx.x, tid = threadIdx.x;
     if (lane >= nl) return;
-    LaneState<ENV> S;
-    load_state<ENV>(S, state, lane, nl);
-    Env<ENV> e(S, g_tables[ENV], P);
     const uint64_t glane = lane_offset + lane;
-    float a[D::ACT];
-    uint64_t ctr = (uint64_t)S.stepCounter * 64u;
-    for (int j = 0; j < D::ACT; ++j)
-        a[j] = actions ? actions[(size_t)lane * D::ACT + j] : (float)(-1.0 + 2.0 * rng_u01(seed, glane, 3, ctr + j));
-    S.stepCounter += 1;
-    float o[D::OBS];
-    double r;
-    int d, kind;
-    e.env_step(a, o, r, d, kind);
-    S.elapsed += 1;
-    int tr = 0;
-    if (max_steps > 0 && S.elapsed >= max_steps) { tr = !d; d = 1; }   // gym TimeLimit
-    if (reward) reward[lane] = (float)r;
-    if (done_out) done_out[lane] = (uint8_t)d;
-    if (trunc_out) trunc_out[lane] = (uint8_t)tr;
-    if (status_out) status_out[lane] = (uint8_t)kind;
+    load_state<ENV>(sh.S, state, lane, tid);
+    __syncthreads();
+    const uint64_t ctr = (uint64_t)sh.S.stepCounter * 64u;
+    if (tid < D::ACT)
+        sh.act[tid] = actions ? actions[(size_t)lane * D::ACT + tid] : (float)(-1.0 + 2.0 * rng_u01(seed, glane, 3, ctr + tid));
+    __syncthreads();
+    if (tid == 0) sh.S.stepCounter += 1;
+    Env<ENV> e(sh, g_tables[ENV], P, tid);
+    e.env_step_coop();
+    if (tid == 0) {
+        sh.S.elapsed += 1;
+        int d = sh.done, tr = 0;
+        if (max_steps > 0 && sh.S.elapsed >= max_steps) { tr = !d; d = 1; }   // gym TimeLimit
+        if (reward) reward[lane] = (float)sh.reward;
+        if (done_out) done_out[lane] = (uint8_t)d;
+        if (trunc_out) trunc_out[lane] = (uint8_t)tr;
+        if (status_out) status_out[lane] = (uint8_t)sh.kind;
+        s_fin = d;
+    }
+    __syncthreads();
     float* orow = obs + (size_t)lane * D::OBS;
-    if (term_obs) for (int k = 0; k < D::OBS; ++k) term_obs[(size_t)lane * D::OBS + k] = o[k];
-    if (d && auto_reset) lane_reset<ENV>(e, S, nullptr, nullptr, orow, lane, seed, glane);
-    else for (int k = 0; k < D::OBS; ++k) orow[k] = o[k];
-    store_state<ENV>(S, state, lane, nl);
+    if (term_obs)
+        for (int k = tid; k < D::OBS; k += BLOCK) term_obs[(size_t)lane * D::OBS + k] = sh.obs[k];
+    if (s_fin && auto_reset) {   // SB3-style auto-reset with device-RNG spawns
+        stage_reset_inputs<ENV>(sh, nullptr, nullptr, lane, tid, seed, glane);
+        e.env_reset_coop();
+    }
+    for (int k = tid; k < D::OBS; k += BLOCK) orow[k] = sh.obs[k];
+    store_state<ENV>(sh.S, state, lane, tid);
 }
 
 __global__ __launch_bounds__(256) void k_sincos(const float* x, float* s, float* c, int n) {
@@ -136,10 +153,9 @@ __global__ __launch_bounds__(256) void k_sincos(const float* x, float* s, float*
 template <int ENV>
 __global__ __launch_bounds__(BLOCK) void k_bodies(const uint32_t* state, int nl, float* out, int32_t* flags) {
     using D = Dims<ENV>;
-    int lane = blockIdx.x * BLOCK + threadIdx.x;
-    if (lane >= nl) return;
-    LaneState<ENV> S;
-    load_state<ENV>(S, state, lane, nl);
+    const int lane = blockIdx.x, tid = threadIdx.x;
+    if (lane >= nl || tid != 0) return;
+    const LaneState<ENV>& S = *reinterpret_cast<const LaneState<ENV>*>(state + (size_t)lane * lane_words<ENV>());
     constexpr int ND = D::NA + D::NB;
     if (out) {
         float* r = out + (size_t)lane * 6 * ND;
@@ -158,7 +174,7 @@ __global__ __launch_bounds__(BLOCK) void k_bodies(const uint32_t* state, int nl,
 // ------------------------------------------------------------------------------ host side
 thread_local std::string g_create_error;
 
-int grid_for(int nl) { return (nl + BLOCK - 1) / BLOCK; }
+int grid_for(int nl) { return nl; }   // one workgroup (wave) per lane
 
 }  // namespace
 
@@ -452,11 +468,8 @@ int mrp_get_state(mrp_ctx* ctx, uint32_t* out) {
     if (!ctx || !out) return MRP_E_ARG;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     size_t nl = (size_t)ctx->n_lanes, nw = (size_t)ctx->words;
-    std::vector<uint32_t> soa(nl * nw);
-    HIPCHK(ctx, hipMemcpyAsync(soa.data(), ctx->d_state, nl * nw * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(out, ctx->d_state, nl * nw * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    for (size_t w = 0; w < nw; ++w)
-        for (size_t l = 0; l < nl; ++l) out[l * nw + w] = soa[w * nl + l];
     return MRP_OK;
 }
 
@@ -464,10 +477,7 @@ int mrp_set_state(mrp_ctx* ctx, const uint32_t* in) {
     if (!ctx || !in) return MRP_E_ARG;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     size_t nl = (size_t)ctx->n_lanes, nw = (size_t)ctx->words;
-    std::vector<uint32_t> soa(nl * nw);
-    for (size_t w = 0; w < nw; ++w)
-        for (size_t l = 0; l < nl; ++l) soa[w * nl + l] = in[l * nw + w];
-    HIPCHK(ctx, hipMemcpyAsync(ctx->d_state, soa.data(), nl * nw * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_state, in, nl * nw * 4, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     ctx->have_reset = 1;
     return MRP_OK;

@@ -85,16 +85,87 @@ template <int ENV> constexpr int lane_words() { return (int)(sizeof(LaneState<EN
 
 struct TOIOut { int state; float t; };
 
+struct ClipV { V2 v; uint32_t id; };
+struct VC {
+    float rAx[2], rAy[2], rBx[2], rBy[2], ni[2], ti[2], nmass[2], tmass[2], vbias[2];
+    float nx, ny, nm0, nm1, nm2, nm3, k0, k1, k2, k3;
+    float mA, mB, iA, iB, friction, restitution;
+    int iaI, ibI, pointCount, slot;
+};
+struct PC {
+    float lpx[2], lpy[2], lnx, lny, lpx0, lpy0;
+    float mA, mB, iA, iB, lcAx, lcAy, lcBx, lcBy, rA, rB;
+    int iaI, ibI, type, pointCount;
+};
+template <int NBODY, int C> struct IslT {
+    int bodies[NBODY];
+    int contacts[C];
+    float pcx[NBODY], pcy[NBODY], pa[NBODY], vvx[NBODY], vvy[NBODY], vw[NBODY];
+    int nb, nc;
+    int index[NBODY];   // body -> island index
+};
+struct SweepV { float lcx, lcy, c0x, c0y, cx, cy, a0, a, alpha0; };
+struct DProxy { const V2* v; int count; float radius; };
+struct SVert { V2 wA, wB, w; float a; int iA, iB; };
+struct Simplex { SVert v[3]; int count; };
+struct SCache { float metric; int count; int iA[3], iB[3]; };
+struct SepFn { int type; V2 lp, axis; };
+
+// Per-lane LDS working set of the cooperative (one wave per world) step.
+template <int ENV> struct Shared {
+    using D = Dims<ENV>;
+    using LS = LaneState<ENV>;
+    static constexpr int ND = LS::ND, NBODY = ND + 4, C = D::CMAX;
+    LS S;
+    VC vcs[C];
+    PC pcs[C];
+    IslT<NBODY, C> isl;
+    int stack[NBODY];
+    float salpha0[4];
+    // collide: contact list snapshot + narrow-phase results (index C is the serial slot)
+    int clist[C];
+    int ccount;
+    uint8_t cover[C];
+    int tpc[C + 1], ttype[C + 1];
+    float tlnx[C + 1], tlny[C + 1], tlpx[C + 1], tlpy[C + 1];
+    float tpx[2][C + 1], tpy[2][C + 1];
+    uint32_t tmid[2][C + 1];
+    // broad phase: active proxy ids (ascending) and per-pair overlap flags
+    int nprox;
+    uint32_t moved;
+    int prox[TREE_N];
+    uint8_t pover[TREE_N * (TREE_N - 1) / 2];
+    // TOI: candidates of one scan (list order) with their post-alpha0-sync sweeps
+    int tn;
+    int tcand[C];
+    SweepV tsA[C], tsB[C];
+    TOIOut tout[C];
+    int plan[C];          // per list position: -1 skip, -2 cached, >=0 candidate index
+    int pslot[C];
+    int np;
+    int toi_done, toi_fnc;
+    // env outputs
+    float obs[D::OBS];
+    double reward;
+    int done, kind;
+    float act[D::ACT];
+    double draws[D::NDRAW];
+};
+
 template <int ENV> struct World {
     using D = Dims<ENV>;
     using LS = LaneState<ENV>;
     static constexpr int NA = D::NA, NB = D::NB, ND = LS::ND, NBODY = ND + 4, NF = D::NF, C = D::CMAX;
 
+    using SH = Shared<ENV>;
+    using Isl = IslT<NBODY, C>;
+    SH& sh;
     LS& S;
     const EnvTables& T;
     const EnvParams& P;
+    const int tid;
 
-    __device__ World(LS& s, const EnvTables& t, const EnvParams& p) : S(s), T(t), P(p) {}
+    __device__ World(SH& s, const EnvTables& t, const EnvParams& p, int thread) : sh(s), S(s.S), T(t), P(p), tid(thread) {}
 
     // ------------------------------------------------------------------ bodies
     __device__ bool is_dyn(int b) const { return b < ND; }
@@ -330,23 +401,40 @@ template <int ENV> struct World {
     }
     // b2BroadPhase::UpdatePairs + AddPair: pairs (lower proxy id, higher id) with at least one
     // moved proxy and overlapping fat AABBs, visited in sorted order == Box2D's sorted pair buffer.
-    __device__ void find_new_contacts() {
-        uint32_t moved = 0;
-        for (int i = 0; i < S.moveCount; ++i) if (S.moveBuf[i] != NULLN) moved |= 1u << S.moveBuf[i];
-        S.moveCount = 0;
-        if (!moved) return;
-        for (int a = 0; a < TREE_N; ++a) {
-            if (S.tud[a] < 0 || !t_leaf(a)) continue;
-            for (int b = a + 1; b < TREE_N; ++b) {
-                if (S.tud[b] < 0 || !t_leaf(b)) continue;
-                if (!(((moved >> a) | (moved >> b)) & 1u)) continue;
-                if (fat_overlap(a, b)) add_pair(S.tud[a], S.tud[b]);
-            }
+    // Cooperative: every thread of the wave calls it; the O(P^2) overlap tests run in parallel,
+    // the order-sensitive AddPair calls run on thread 0 in sorted order.
+    __device__ void find_new_contacts_coop() {
+        if (tid == 0) {
+            uint32_t moved = 0;
+            for (int i = 0; i < S.moveCount; ++i) if (S.moveBuf[i] != NULLN) moved |= 1u << S.moveBuf[i];
+            S.moveCount = 0;
+            int n = 0;
+            if (moved)
+                for (int a = 0; a < TREE_N; ++a) if (S.tud[a] >= 0 && t_leaf(a)) sh.prox[n++] = a;
+            sh.nprox = n;
+            sh.moved = moved;
         }
+        __syncthreads();
+        const int n = sh.nprox;
+        const uint32_t moved = sh.moved;
+        const int npairs = n * (n - 1) / 2;
+        for (int p = tid; p < npairs; p += 64) {
+            int i = 0, q = p;
+            while (q >= n - 1 - i) { q -= n - 1 - i; ++i; }
+            int a = sh.prox[i], b = sh.prox[i + 1 + q];
+            sh.pover[p] = ((((moved >> a) | (moved >> b)) & 1u) && fat_overlap(a, b)) ? 1 : 0;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int p = 0;
+            for (int i = 0; i < n; ++i)
+                for (int j = i + 1; j < n; ++j, ++p)
+                    if (sh.pover[p]) add_pair(S.tud[sh.prox[i]], S.tud[sh.prox[j]]);
+        }
+        __syncthreads();
     }
 
     // ---------------------------------------------------------------- narrow phase (b2CollidePolygons)
-    struct ClipV { V2 v; uint32_t id; };
     __device__ static uint32_t cf_make(int iA, int iB, int tA, int tB) {
         return (uint32_t)(uint8_t)iA | ((uint32_t)(uint8_t)iB << 8) | ((uint32_t)(uint8_t)tA << 16) | ((uint32_t)(uint8_t)tB << 24);
     }
@@ -363,23 +451,24 @@ template <int ENV> struct World {
         edge = best;
         return maxSep;
     }
-    __device__ static int clip(ClipV out[2], const ClipV in[2], V2 normal, float offset, int vertexIndexA) {
+    // b2ClipSegmentToLine with the two in/out vertices kept in registers
+    __device__ static int clip(ClipV& o0, ClipV& o1, const ClipV& i0, const ClipV& i1, V2 normal, float offset, int vertexIndexA) {
         int numOut = 0;
-        float d0 = vdot(normal, in[0].v) - offset;
-        float d1 = vdot(normal, in[1].v) - offset;
-        if (d0 <= 0.0f) out[numOut++] = in[0];
-        if (d1 <= 0.0f) out[numOut++] = in[1];
-        if (d0 * d1 < 0.0f) {
+        float d0 = vdot(normal, i0.v) - offset;
+        float d1 = vdot(normal, i1.v) - offset;
+        if (d0 <= 0.0f) { o0 = i0; numOut = 1; }
+        if (d1 <= 0.0f) { if (numOut == 0) o0 = i1; else o1 = i1; ++numOut; }
+        if (d0 * d1 < 0.0f) {   // exactly one endpoint was kept, so this fills slot 1
             float interp = d0 / (d0 - d1);
-            out[numOut].v = vadd(in[0].v, vmul(interp, vsub(in[1].v, in[0].v)));
-            out[numOut].id = cf_make(vertexIndexA, (int)((in[0].id >> 8) & 0xff), 0, 1);
+            o1.v = vadd(i0.v, vmul(interp, vsub(i1.v, i0.v)));
+            o1.id = cf_make(vertexIndexA, (int)((i0.id >> 8) & 0xff), 0, 1);
             ++numOut;
         }
         return numOut;
     }
-    // writes the manifold of slot c
-    __device__ void collide_polygons(int c, const ShapeDef& pA, Xf xA, const ShapeDef& pB, Xf xB) {
-        S.mpc[c] = 0;
+    // b2CollidePolygons into manifold scratch slot k (sh.t*[k])
+    __device__ void collide_polygons(int k, const ShapeDef& pA, Xf xA, const ShapeDef& pB, Xf xB) {
+        sh.tpc[k] = 0;
         float totalRadius = pA.radius + pB.radius;
         int edgeA = 0;
         float sepA = find_max_separation(edgeA, pA, xA, pB, xB);
@@ -393,16 +482,15 @@ template <int ENV> struct World {
         const ShapeDef& p2 = flip ? pA : pB;
         Xf x1 = flip ? xB : xA, x2 = flip ? xA : xB;
         int edge1 = flip ? edgeB : edgeA;
-        S.mtype[c] = flip ? MT_FACEB : MT_FACEA;
-        // incident edge
-        ClipV inc[2];
+        sh.ttype[k] = flip ? MT_FACEB : MT_FACEA;
+        ClipV inc0, inc1;   // incident edge
         {
             V2 normal1 = mulT_rv(x2.q, mul_rv(x1.q, p1.n[edge1]));
             int index = 0; float minDot = FLT_MAXV;
             for (int i = 0; i < p2.count; ++i) { float d = vdot(normal1, p2.n[i]); if (d < minDot) { minDot = d; index = i; } }
             int i1 = index, i2 = i1 + 1 < p2.count ? i1 + 1 : 0;
-            inc[0].v = mul_xv(x2, p2.v[i1]); inc[0].id = cf_make(edge1, i1, 1, 0);
-            inc[1].v = mul_xv(x2, p2.v[i2]); inc[1].id = cf_make(edge1, i2, 1, 0);
+            inc0.v = mul_xv(x2, p2.v[i1]); inc0.id = cf_make(edge1, i1, 1, 0);
+            inc1.v = mul_xv(x2, p2.v[i2]); inc1.id = cf_make(edge1, i2, 1, 0);
         }
         int iv1 = edge1, iv2 = edge1 + 1 < p1.count ? edge1 + 1 : 0;
         V2 v11 = p1.v[iv1], v12 = p1.v[iv2];
@@ -416,77 +504,93 @@ template <int ENV> struct World {
         float frontOffset = vdot(normal, v11);
         float side1 = -vdot(tangent, v11) + totalRadius;
         float side2 = vdot(tangent, v12) + totalRadius;
-        ClipV cp1[2], cp2[2];
-        if (clip(cp1, inc, vneg(tangent), side1, iv1) < 2) return;
-        if (clip(cp2, cp1, tangent, side2, iv2) < 2) return;
-        S.mlnx[c] = localNormal.x; S.mlny[c] = localNormal.y;
-        S.mlpx[c] = planePoint.x; S.mlpy[c] = planePoint.y;
+        ClipV a0, a1, b0, b1;
+        if (clip(a0, a1, inc0, inc1, vneg(tangent), side1, iv1) < 2) return;
+        if (clip(b0, b1, a0, a1, tangent, side2, iv2) < 2) return;
+        sh.tlnx[k] = localNormal.x; sh.tlny[k] = localNormal.y;
+        sh.tlpx[k] = planePoint.x; sh.tlpy[k] = planePoint.y;
         int pc = 0;
+#pragma unroll
         for (int i = 0; i < 2; ++i) {
-            float sep = vdot(normal, cp2[i].v) - frontOffset;
+            const ClipV& cv = i == 0 ? b0 : b1;
+            float sep = vdot(normal, cv.v) - frontOffset;
             if (sep <= totalRadius) {
-                V2 lp = mulT_xv(x2, cp2[i].v);
-                uint32_t id = cp2[i].id;
+                V2 lp = mulT_xv(x2, cv.v);
+                uint32_t id = cv.id;
                 if (flip) {
-                    uint32_t a0 = id & 0xff, b0 = (id >> 8) & 0xff, ta = (id >> 16) & 0xff, tb = (id >> 24) & 0xff;
-                    id = b0 | (a0 << 8) | (tb << 16) | (ta << 24);
+                    uint32_t q0 = id & 0xff, q1 = (id >> 8) & 0xff, ta = (id >> 16) & 0xff, tb = (id >> 24) & 0xff;
+                    id = q1 | (q0 << 8) | (tb << 16) | (ta << 24);
                 }
-                S.mpx[pc][c] = lp.x; S.mpy[pc][c] = lp.y; S.mid[pc][c] = id;
+                if (pc == 0) { sh.tpx[0][k] = lp.x; sh.tpy[0][k] = lp.y; sh.tmid[0][k] = id; }
+                else { sh.tpx[1][k] = lp.x; sh.tpy[1][k] = lp.y; sh.tmid[1][k] = id; }
                 ++pc;
             }
         }
-        S.mpc[c] = pc;
+        sh.tpc[k] = pc;
     }
-    // b2Contact::Update
-    __device__ void contact_update(int c) {
+    // second half of b2Contact::Update: adopt manifold scratch slot k, match feature ids to
+    // carry the warm-start impulses, update the touching flag, fire Begin/End events
+    __device__ void contact_commit(int c, int k) {
         int oldCount = S.mpc[c];
         uint32_t oid0 = S.mid[0][c], oid1 = S.mid[1][c];
         float on0 = S.mni[0][c], on1 = S.mni[1][c], ot0 = S.mti[0][c], ot1 = S.mti[1][c];
         S.cflags[c] |= CF_ENABLED;
         bool wasTouching = (S.cflags[c] & CF_TOUCHING) != 0;
-        int fa = S.cfa[c], fb = S.cfb[c];
-        collide_polygons(c, T.shape[fa], xf(T.fix_body[fa]), T.shape[fb], xf(T.fix_body[fb]));
-        bool touching = S.mpc[c] > 0;
-        for (int i = 0; i < S.mpc[c]; ++i) {
-            uint32_t id2 = S.mid[i][c];
+        int pcount = sh.tpc[k];
+        S.mpc[c] = pcount;
+        if (pcount > 0) {
+            S.mtype[c] = sh.ttype[k];
+            S.mlnx[c] = sh.tlnx[k]; S.mlny[c] = sh.tlny[k]; S.mlpx[c] = sh.tlpx[k]; S.mlpy[c] = sh.tlpy[k];
+        }
+        for (int i = 0; i < pcount; ++i) {
+            uint32_t id2 = sh.tmid[i][k];
+            S.mpx[i][c] = sh.tpx[i][k]; S.mpy[i][c] = sh.tpy[i][k]; S.mid[i][c] = id2;
             float ni = 0.0f, ti = 0.0f;
             if (oldCount > 0 && oid0 == id2) { ni = on0; ti = ot0; }
             else if (oldCount > 1 && oid1 == id2) { ni = on1; ti = ot1; }
             S.mni[i][c] = ni; S.mti[i][c] = ti;
         }
+        bool touching = pcount > 0;
         if (touching) S.cflags[c] |= CF_TOUCHING; else S.cflags[c] &= ~CF_TOUCHING;
         if (!wasTouching && touching) contact_event(c, 1);
         if (wasTouching && !touching) contact_event(c, 0);
     }
-    __device__ void collide() {   // b2ContactManager::Collide
-        int c = S.cHead;
-        while (c != NULLN) {
-            int next = S.cnext[c];
-            if (!fat_overlap(S.proxy[S.cfa[c]], S.proxy[S.cfb[c]])) { destroy_contact(c, true); c = next; continue; }
-            contact_update(c);
-            c = next;
+    // b2Contact::Update on one contact (serial callers: TOI)
+    __device__ void contact_update(int c) {
+        int fa = S.cfa[c], fb = S.cfb[c];
+        collide_polygons(C, T.shape[fa], xf(T.fix_body[fa]), T.shape[fb], xf(T.fix_body[fb]));
+        contact_commit(c, C);
+    }
+    // b2ContactManager::Collide.  Cooperative: thread 0 snapshots the contact list, all threads
+    // run the broad-phase overlap test + SAT narrow phase of one contact each, then thread 0
+    // destroys / commits in list order (events fire in the reference's order).
+    __device__ void collide_coop() {
+        if (tid == 0) {
+            int n = 0;
+            for (int c = S.cHead; c != NULLN; c = S.cnext[c]) sh.clist[n++] = c;
+            sh.ccount = n;
         }
+        __syncthreads();
+        const int n = sh.ccount;
+        for (int i = tid; i < n; i += 64) {
+            int c = sh.clist[i];
+            int fa = S.cfa[c], fb = S.cfb[c];
+            bool ov = fat_overlap(S.proxy[fa], S.proxy[fb]);
+            sh.cover[i] = ov ? 1 : 0;
+            if (ov) collide_polygons(i, T.shape[fa], xf(T.fix_body[fa]), T.shape[fb], xf(T.fix_body[fb]));
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int i = 0; i < n; ++i) {
+                int c = sh.clist[i];
+                if (!sh.cover[i]) destroy_contact(c, true);
+                else contact_commit(c, i);
+            }
+        }
+        __syncthreads();
     }
 
     // ---------------------------------------------------------------- contact solver
-    struct VC {
-        float rAx[2], rAy[2], rBx[2], rBy[2], ni[2], ti[2], nmass[2], tmass[2], vbias[2];
-        float nx, ny, nm0, nm1, nm2, nm3, k0, k1, k2, k3;
-        float mA, mB, iA, iB, friction, restitution;
-        int iaI, ibI, pointCount, slot;
-    };
-    struct PC {
-        float lpx[2], lpy[2], lnx, lny, lpx0, lpy0;
-        float mA, mB, iA, iB, lcAx, lcAy, lcBx, lcBy, rA, rB;
-        int iaI, ibI, type, pointCount;
-    };
-    struct Isl {
-        int bodies[NBODY];
-        int contacts[C];
-        float pcx[NBODY], pcy[NBODY], pa[NBODY], vvx[NBODY], vvy[NBODY], vw[NBODY];
-        int nb, nc;
-        int index[NBODY];   // body -> island index
-    };
     __device__ float body_invMass(int b) const { return T.invMass[b]; }
     __device__ float body_invI(int b) const { return T.invI[b]; }
 
@@ -802,21 +906,19 @@ template <int ENV> struct World {
         }
     }
 
-    // b2World::Solve
-    __device__ void solve(float h, float dtRatio) {
-        Isl is;
-        VC vcs[C];
-        PC pcs[C];
-        bool bflag[NBODY];
-        for (int b = 0; b < NBODY; ++b) bflag[b] = false;
+    // b2World::Solve, serial part (thread 0): island DFS + island solves + SynchronizeFixtures.
+    // The trailing FindNewContacts is cooperative and issued by world_step_coop.
+    __device__ void solve_serial(float h, float dtRatio) {
+        Isl& is = sh.isl;
+        uint32_t bflag = 0;   // body island flags (bit per body)
         for (int c = S.cHead; c != NULLN; c = S.cnext[c]) S.cflags[c] &= ~CF_ISLAND;
-        int stack[NBODY];
+        int* stack = sh.stack;
         // body list = reverse creation order: walls (static, never seeds), agents, blocks
         for (int seed = ND - 1; seed >= 0; --seed) {
-            if (bflag[seed]) continue;
+            if (bflag & (1u << seed)) continue;
             is.nb = 0; is.nc = 0;
             int sc = 0;
-            stack[sc++] = seed; bflag[seed] = true;
+            stack[sc++] = seed; bflag |= 1u << seed;
             while (sc > 0) {
                 int b = stack[--sc];
                 island_add_body(is, b);
@@ -829,19 +931,17 @@ template <int ENV> struct World {
                     is.contacts[is.nc++] = c;
                     S.cflags[c] |= CF_ISLAND;
                     int other = bA == b ? bB : bA;
-                    if (bflag[other]) continue;
-                    stack[sc++] = other; bflag[other] = true;
+                    if (bflag & (1u << other)) continue;
+                    stack[sc++] = other; bflag |= 1u << other;
                 }
             }
-            island_solve(is, h, dtRatio, vcs, pcs);
-            for (int i = 0; i < is.nb; ++i) if (!is_dyn(is.bodies[i])) bflag[is.bodies[i]] = false;
+            island_solve(is, h, dtRatio, sh.vcs, sh.pcs);
+            for (int i = 0; i < is.nb; ++i) if (!is_dyn(is.bodies[i])) bflag &= ~(1u << is.bodies[i]);
         }
-        for (int b = ND - 1; b >= 0; --b) if (bflag[b]) sync_fixtures(b);
-        find_new_contacts();
+        for (int b = ND - 1; b >= 0; --b) if (bflag & (1u << b)) sync_fixtures(b);
     }
 
     // ---------------------------------------------------------------- TOI
-    struct SweepV { float lcx, lcy, c0x, c0y, cx, cy, a0, a, alpha0; };
     __device__ SweepV sweep(int b, const float* salpha0) const {
         SweepV s;
         if (b < ND) { s.lcx = T.lcx[b]; s.lcy = T.lcy[b]; s.c0x = S.c0x[b]; s.c0y = S.c0y[b]; s.cx = S.cx[b]; s.cy = S.cy[b]; s.a0 = S.a0[b]; s.a = S.a[b]; s.alpha0 = S.alpha0[b]; }
@@ -875,15 +975,11 @@ template <int ENV> struct World {
         if (b < ND) sync_transform(b);
     }
 
-    struct DProxy { const V2* v; int count; float radius; };
     __device__ static int support(const DProxy& p, V2 d) {
         int best = 0; float bv = vdot(p.v[0], d);
         for (int i = 1; i < p.count; ++i) { float val = vdot(p.v[i], d); if (val > bv) { best = i; bv = val; } }
         return best;
     }
-    struct SVert { V2 wA, wB, w; float a; int iA, iB; };
-    struct Simplex { SVert v[3]; int count; };
-    struct SCache { float metric; int count; int iA[3], iB[3]; };
     __device__ static float s_metric(const Simplex& s) {
         if (s.count == 2) return vlen(vsub(s.v[0].w, s.v[1].w));
         if (s.count == 3) return vcross(vsub(s.v[1].w, s.v[0].w), vsub(s.v[2].w, s.v[0].w));
@@ -977,7 +1073,6 @@ template <int ENV> struct World {
         for (int i = 0; i < s.count; ++i) { cache.iA[i] = s.v[i].iA; cache.iB[i] = s.v[i].iB; }
         return dist;
     }
-    struct SepFn { int type; V2 lp, axis; };
     __device__ static float sep_eval(const SepFn& f, const DProxy& pA, const DProxy& pB, const SweepV& sA, const SweepV& sB, int iA, int iB, float t) {
         Xf xA = sweep_xf(sA, t), xB = sweep_xf(sB, t);
         if (f.type == 0) return vdot(vsub(mul_xv(xB, pB.v[iB]), mul_xv(xA, pA.v[iA])), f.axis);
@@ -1115,118 +1210,160 @@ template <int ENV> struct World {
         }
     }
 
-    // b2World::SolveTOI
-    __device__ void solve_toi(float dt) {
-        float salpha0[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        for (int b = 0; b < ND; ++b) S.alpha0[b] = 0.0f;
-        for (int c = S.cHead; c != NULLN; c = S.cnext[c]) { S.cflags[c] &= ~(CF_TOI | CF_ISLAND); S.ctoiCount[c] = 0; S.ctoi[c] = 1.0f; }
-        Isl is;
-        VC vcs[MAX_TOI_CONTACTS];
-        PC pcs[MAX_TOI_CONTACTS];
-        bool bflag[NBODY];
-        for (int b = 0; b < NBODY; ++b) bflag[b] = false;
-        for (;;) {
-            int minC = NULLN; float minAlpha = 1.0f;
-            for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
-                if ((S.cflags[c] & CF_ENABLED) == 0) continue;
-                if (S.ctoiCount[c] > MAX_SUBSTEPS) continue;
-                float alpha = 1.0f;
-                if (S.cflags[c] & CF_TOI) {
-                    alpha = S.ctoi[c];
-                } else {
-                    int fa = S.cfa[c], fb = S.cfb[c];
-                    int bA = T.fix_body[fa], bB = T.fix_body[fb];
-                    bool collideA = !is_dyn(bA), collideB = !is_dyn(bB);   // no bullets in these envs
-                    if (!collideA && !collideB) continue;
-                    SweepV sA = sweep(bA, salpha0), sB = sweep(bB, salpha0);
-                    float alpha0 = sA.alpha0;
-                    if (sA.alpha0 < sB.alpha0) { alpha0 = sB.alpha0; sweep_advance(sA, alpha0); sweep_store(bA, sA, salpha0); }
-                    else if (sB.alpha0 < sA.alpha0) { alpha0 = sA.alpha0; sweep_advance(sB, alpha0); sweep_store(bB, sB, salpha0); }
-                    DProxy pA = { T.shape[fa].v, T.shape[fa].count, T.shape[fa].radius };
-                    DProxy pB = { T.shape[fb].v, T.shape[fb].count, T.shape[fb].radius };
-                    TOIOut o = time_of_impact(pA, pB, sA, sB);
-                    if (o.state == 3) alpha = fmin_(alpha0 + (1.0f - alpha0) * o.t, 1.0f);
-                    else alpha = 1.0f;
-                    S.ctoi[c] = alpha;
-                    S.cflags[c] |= CF_TOI;
-                }
-                if (alpha < minAlpha) { minC = c; minAlpha = alpha; }
-            }
-            if (minC == NULLN || 1.0f - 10.0f * FLT_EPS < minAlpha) break;
-            ++S.toiEvents;
-            int fa = S.cfa[minC], fb = S.cfb[minC];
+    // b2World::SolveTOI, cooperative.  Each pass of the event loop: thread 0 walks the contact
+    // list in order, applying the alpha0 synchronisation (which mutates sweeps exactly as the
+    // reference's scan does) and snapshotting the sweeps of every contact whose TOI must be
+    // computed; all threads then run b2TimeOfImpact on one candidate each; thread 0 takes the
+    // minimum in list order and processes the event serially.
+    __device__ void toi_scan() {
+        float* salpha0 = sh.salpha0;
+        int tn = 0, np = 0;
+        for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
+            if ((S.cflags[c] & CF_ENABLED) == 0) continue;
+            if (S.ctoiCount[c] > MAX_SUBSTEPS) continue;
+            if (S.cflags[c] & CF_TOI) { sh.plan[np] = -2; sh.pslot[np++] = c; continue; }
+            int fa = S.cfa[c], fb = S.cfb[c];
             int bA = T.fix_body[fa], bB = T.fix_body[fb];
-            SweepV back1 = sweep(bA, salpha0), back2 = sweep(bB, salpha0);
-            body_advance(bA, minAlpha, salpha0);
-            body_advance(bB, minAlpha, salpha0);
-            contact_update(minC);
-            S.cflags[minC] &= ~CF_TOI;
-            ++S.ctoiCount[minC];
-            if ((S.cflags[minC] & CF_ENABLED) == 0 || (S.cflags[minC] & CF_TOUCHING) == 0) {
-                S.cflags[minC] &= ~CF_ENABLED;
-                sweep_store(bA, back1, salpha0); sweep_store(bB, back2, salpha0);
-                if (bA < ND) sync_transform(bA);
-                if (bB < ND) sync_transform(bB);
-                continue;
+            bool collideA = !is_dyn(bA), collideB = !is_dyn(bB);   // no bullets in these envs
+            if (!collideA && !collideB) continue;
+            SweepV sA = sweep(bA, salpha0), sB = sweep(bB, salpha0);
+            if (sA.alpha0 < sB.alpha0) { sweep_advance(sA, sB.alpha0); sweep_store(bA, sA, salpha0); }
+            else if (sB.alpha0 < sA.alpha0) { sweep_advance(sB, sA.alpha0); sweep_store(bB, sB, salpha0); }
+            sh.tcand[tn] = c; sh.tsA[tn] = sA; sh.tsB[tn] = sB;
+            sh.plan[np] = tn; sh.pslot[np++] = c;
+            ++tn;
+        }
+        sh.tn = tn; sh.np = np;
+    }
+    // returns true when an event was processed that needs FindNewContacts
+    __device__ void toi_event(float dt) {
+        float* salpha0 = sh.salpha0;
+        int minC = NULLN; float minAlpha = 1.0f;
+        for (int k = 0; k < sh.np; ++k) {
+            int c = sh.pslot[k];
+            float alpha;
+            if (sh.plan[k] == -2) alpha = S.ctoi[c];
+            else {
+                int i = sh.plan[k];
+                float alpha0 = sh.tsA[i].alpha0;   // both sweeps share alpha0 after the sync
+                TOIOut o = sh.tout[i];
+                if (o.state == 3) alpha = fmin_(alpha0 + (1.0f - alpha0) * o.t, 1.0f);
+                else alpha = 1.0f;
+                S.ctoi[c] = alpha;
+                S.cflags[c] |= CF_TOI;
             }
-            is.nb = 0; is.nc = 0;
-            island_add_body(is, bA); island_add_body(is, bB);
-            is.contacts[is.nc++] = minC;
-            bflag[bA] = true; bflag[bB] = true;
-            S.cflags[minC] |= CF_ISLAND;
-            int pair[2] = {bA, bB};
-            for (int k = 0; k < 2; ++k) {
-                int body = pair[k];
-                if (!is_dyn(body)) continue;
-                for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
-                    int cA = T.fix_body[S.cfa[c]], cB = T.fix_body[S.cfb[c]];
-                    if (cA != body && cB != body) continue;
-                    if (is.nb == 2 * MAX_TOI_CONTACTS) break;
-                    if (is.nc == MAX_TOI_CONTACTS) break;
-                    if (S.cflags[c] & CF_ISLAND) continue;
-                    int other = cA == body ? cB : cA;
-                    if (is_dyn(other)) continue;   // only static (no bullets/kinematic here)
-                    SweepV backup = sweep(other, salpha0);
-                    if (!bflag[other]) body_advance(other, minAlpha, salpha0);
-                    contact_update(c);
-                    if ((S.cflags[c] & CF_ENABLED) == 0 || (S.cflags[c] & CF_TOUCHING) == 0) {
-                        sweep_store(other, backup, salpha0);
-                        if (other < ND) sync_transform(other);
-                        continue;
-                    }
-                    S.cflags[c] |= CF_ISLAND;
-                    is.contacts[is.nc++] = c;
-                    if (bflag[other]) continue;
-                    bflag[other] = true;
-                    island_add_body(is, other);
+            if (alpha < minAlpha) { minC = c; minAlpha = alpha; }
+        }
+        sh.toi_fnc = 0;
+        if (minC == NULLN || 1.0f - 10.0f * FLT_EPS < minAlpha) { sh.toi_done = 1; return; }
+        ++S.toiEvents;
+        int fa = S.cfa[minC], fb = S.cfb[minC];
+        int bA = T.fix_body[fa], bB = T.fix_body[fb];
+        SweepV back1 = sweep(bA, salpha0), back2 = sweep(bB, salpha0);
+        body_advance(bA, minAlpha, salpha0);
+        body_advance(bB, minAlpha, salpha0);
+        contact_update(minC);
+        S.cflags[minC] &= ~CF_TOI;
+        ++S.ctoiCount[minC];
+        if ((S.cflags[minC] & CF_ENABLED) == 0 || (S.cflags[minC] & CF_TOUCHING) == 0) {
+            S.cflags[minC] &= ~CF_ENABLED;
+            sweep_store(bA, back1, salpha0); sweep_store(bB, back2, salpha0);
+            if (bA < ND) sync_transform(bA);
+            if (bB < ND) sync_transform(bB);
+            return;   // no FindNewContacts on this path (reference `continue`)
+        }
+        Isl& is = sh.isl;
+        uint32_t bflag = 0;
+        is.nb = 0; is.nc = 0;
+        island_add_body(is, bA); island_add_body(is, bB);
+        is.contacts[is.nc++] = minC;
+        bflag |= (1u << bA) | (1u << bB);
+        S.cflags[minC] |= CF_ISLAND;
+        const int pair[2] = {bA, bB};
+        for (int k = 0; k < 2; ++k) {
+            int body = pair[k];
+            if (!is_dyn(body)) continue;
+            for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
+                int cA = T.fix_body[S.cfa[c]], cB = T.fix_body[S.cfb[c]];
+                if (cA != body && cB != body) continue;
+                if (is.nb == 2 * MAX_TOI_CONTACTS) break;
+                if (is.nc == MAX_TOI_CONTACTS) break;
+                if (S.cflags[c] & CF_ISLAND) continue;
+                int other = cA == body ? cB : cA;
+                if (is_dyn(other)) continue;   // only static bodies join a TOI island here
+                SweepV backup = sweep(other, salpha0);
+                if (!(bflag & (1u << other))) body_advance(other, minAlpha, salpha0);
+                contact_update(c);
+                if ((S.cflags[c] & CF_ENABLED) == 0 || (S.cflags[c] & CF_TOUCHING) == 0) {
+                    sweep_store(other, backup, salpha0);
+                    if (other < ND) sync_transform(other);
+                    continue;
                 }
+                S.cflags[c] |= CF_ISLAND;
+                is.contacts[is.nc++] = c;
+                if (bflag & (1u << other)) continue;
+                bflag |= 1u << other;
+                island_add_body(is, other);
             }
-            island_solve_toi(is, (1.0f - minAlpha) * dt, is.index[bA], is.index[bB], vcs, pcs, salpha0);
-            for (int i = 0; i < is.nb; ++i) {
-                int body = is.bodies[i];
-                bflag[body] = false;
-                if (!is_dyn(body)) continue;
-                sync_fixtures(body);
-                for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
-                    int cA = T.fix_body[S.cfa[c]], cB = T.fix_body[S.cfb[c]];
-                    if (cA == body || cB == body) S.cflags[c] &= ~(CF_TOI | CF_ISLAND);
-                }
+        }
+        island_solve_toi(is, (1.0f - minAlpha) * dt, is.index[bA], is.index[bB], sh.vcs, sh.pcs, salpha0);
+        for (int i = 0; i < is.nb; ++i) {
+            int body = is.bodies[i];
+            if (!is_dyn(body)) continue;
+            sync_fixtures(body);
+            for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
+                int cA = T.fix_body[S.cfa[c]], cB = T.fix_body[S.cfb[c]];
+                if (cA == body || cB == body) S.cflags[c] &= ~(CF_TOI | CF_ISLAND);
             }
-            find_new_contacts();
+        }
+        sh.toi_fnc = 1;
+    }
+    __device__ void solve_toi_coop(float dt) {
+        if (tid == 0) {
+            for (int i = 0; i < 4; ++i) sh.salpha0[i] = 0.0f;
+            for (int b = 0; b < ND; ++b) S.alpha0[b] = 0.0f;
+            for (int c = S.cHead; c != NULLN; c = S.cnext[c]) { S.cflags[c] &= ~(CF_TOI | CF_ISLAND); S.ctoiCount[c] = 0; S.ctoi[c] = 1.0f; }
+            sh.toi_done = 0;
+        }
+        for (;;) {
+            if (tid == 0) toi_scan();
+            __syncthreads();
+            const int tn = sh.tn;
+            for (int i = tid; i < tn; i += 64) {
+                int c = sh.tcand[i];
+                int fa = S.cfa[c], fb = S.cfb[c];
+                DProxy pA = {T.shape[fa].v, T.shape[fa].count, T.shape[fa].radius};
+                DProxy pB = {T.shape[fb].v, T.shape[fb].count, T.shape[fb].radius};
+                sh.tout[i] = time_of_impact(pA, pB, sh.tsA[i], sh.tsB[i]);
+            }
+            __syncthreads();
+            if (tid == 0) toi_event(dt);
+            __syncthreads();
+            if (sh.toi_done) break;
+            if (sh.toi_fnc) find_new_contacts_coop();
         }
     }
 
-    // b2World::Step(1/50, 180, 60)
-    __device__ void world_step() {
+    // b2World::Step(1/50, 180, 60), cooperative (every thread of the wave calls it)
+    __device__ void world_step_coop() {
         const float dt = 1.0f / 50;
-        if (S.newFixture) { find_new_contacts(); S.newFixture = 0; }
+        if (S.newFixture) {
+            __syncthreads();
+            if (tid == 0) S.newFixture = 0;
+            find_new_contacts_coop();   // begins with a barrier-separated read of moveBuf
+        }
         float inv_dt = 1.0f / dt;
         float dtRatio = S.inv_dt0 * dt;
-        collide();
-        solve(dt, dtRatio);
-        solve_toi(dt);
-        S.inv_dt0 = inv_dt;
-        for (int b = 0; b < ND; ++b) { S.fx[b] = 0.0f; S.fy[b] = 0.0f; S.tq[b] = 0.0f; }
+        collide_coop();
+        if (tid == 0) solve_serial(dt, dtRatio);
+        __syncthreads();
+        find_new_contacts_coop();
+        solve_toi_coop(dt);
+        if (tid == 0) {
+            S.inv_dt0 = inv_dt;
+            for (int b = 0; b < ND; ++b) { S.fx[b] = 0.0f; S.fy[b] = 0.0f; S.tq[b] = 0.0f; }
+        }
+        __syncthreads();
     }
 };
 

@@ -1258,7 +1258,7 @@ static void island_solve(Island* is, World* w, TimeStep step) {
     solver_init_velocity_constraints(&s);
     if (step.warmStarting) solver_warm_start(&s);
     for (int i = 0; i < step.velocityIterations; ++i) solver_solve_velocity(&s);
-    w->velIters += step.velocityIterations;
+    w->velIters += (long)step.velocityIterations * is->contactCount;
     solver_store_impulses(&s);
     integrate_positions(is, h, 0);
     for (int i = 0; i < step.positionIterations; ++i) {

@@ -536,6 +536,7 @@ void or_get_flags(const OrEnv* e, int* gc, int* bip) {
 }
 int or_contact_count(const OrEnv* e) { return e->world->cm.contactCount; }
 void or_counters(const OrEnv* e, long* toi, long* pos) { *toi = e->world->toiEvents; *pos = e->world->posIters; }
+long or_vel_constraint_iters(const OrEnv* e) { return e->world->velIters; }
 static int push_proxies(const Body* b, int* out, int k) {
     /* creation order == reverse fixture-list order */
     int n = 0; const Fixture* fs[8];
