@@ -31,7 +31,7 @@ EXPORTED = (
     "mrp_set_stream", "mrp_synchronize", "mrp_set_reward_params", "mrp_update_params", "mrp_update_goal",
     "mrp_reset", "mrp_reset_device", "mrp_step", "mrp_step_device", "mrp_set_auto_reset",
     "mrp_get_bodies", "mrp_get_flags", "mrp_counters", "mrp_state_words", "mrp_get_state", "mrp_set_state",
-    "mrp_set_time_limit", "mrp_selftest_sincos",
+    "mrp_set_time_limit", "mrp_selftest_sincos", "mrp_debug_stamps",
 )
 
 _lib = None
@@ -41,14 +41,15 @@ class MrpError(RuntimeError):
     pass
 
 
-def load() -> ctypes.CDLL:
+def load(path: str | None = None) -> ctypes.CDLL:
     """Load libmrp.so (raises if it has not been built: there is no CPU fallback)."""
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
+    LIB_PATH_ = path or os.environ.get("MRP_LIB") or LIB_PATH
+    if not os.path.exists(LIB_PATH_):
         raise MrpError(f"{LIB_PATH} not built; run `python -m gym_puzzles_amd.build` (hipcc, gfx950)")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH_)
     i, d, u64, P = ctypes.c_int, ctypes.c_double, ctypes.c_uint64, ctypes.c_void_p
     ip = ctypes.POINTER(ctypes.c_int)
     L.mrp_env_dims.argtypes = [i, ip, ip, ip, ip, ip, ip]
@@ -77,6 +78,7 @@ def load() -> ctypes.CDLL:
     L.mrp_set_state.argtypes = [P, P]
     L.mrp_set_time_limit.argtypes = [P, i]
     L.mrp_selftest_sincos.argtypes = [i, P, P, P, i]
+    L.mrp_debug_stamps.argtypes = [i, P]
     _lib = L
     return L
 

@@ -34,16 +34,20 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(d) <= t for d in DEPS if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
-        return OUT
-    cmd = [hipcc()] + FLAGS + SOURCES + ["-o", OUT + ".tmp"]
+def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
+    """Build libmrp.so (or a diagnostic variant with extra -D defines into ``out``)."""
+    if not force and out == OUT and up_to_date():
+        return out
+    cmd = [hipcc()] + FLAGS + [f"-D{d}" for d in defines] + SOURCES + ["-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    if "--stamps" in sys.argv:   # diagnostic per-phase timing build (tools/phase_profile.py)
+        print(build(force=True, verbose=True, out=os.path.join(HERE, "libmrp_stamps.so"), defines=("MRP_STAMPS",)))
+    else:
+        print(build(force="--force" in sys.argv, verbose=True))

@@ -30,9 +30,9 @@ template <int ENV> struct Env : World<ENV> {
     using W::S; using W::T; using W::P; using W::sh; using W::tid;
     static constexpr int NA = D::NA, NB = D::NB, ND = W::ND, NF = D::NF;
 
-    __device__ Env(typename W::SH& s, const EnvTables& t, const EnvParams& p, int thread) : W(s, t, p, thread) {}
+    __device__ __forceinline__ Env(typename W::SH& s, const EnvTables& t, const EnvParams& p, int thread) : W(s, t, p, thread) {}
 
-    __device__ void init_empty_world() {   // fresh b2World (Box2D.b2World(gravity=(0,0), doSleep=False))
+    __device__ __forceinline__ void init_empty_world() {   // fresh b2World (Box2D.b2World(gravity=(0,0), doSleep=False))
         for (int i = 0; i < TREE_N; ++i) { S.tpar[i] = i + 1 < TREE_N ? i + 1 : NULLN; S.th[i] = -1; S.tud[i] = -1; S.tc1[i] = NULLN; S.tc2[i] = NULLN; }
         S.root = NULLN; S.freeList = 0; S.nodeCount = 0; S.moveCount = 0;
         S.cHead = NULLN; S.cFree = 0; S.cCount = 0;
@@ -44,7 +44,7 @@ template <int ENV> struct Env : World<ENV> {
 
     // _destroy (multi_robot_puzzle_00.py:218-229): blocks, walls, agents; each body's proxies
     // in fixture-list order (newest first).  The listener is detached, so no End events.
-    __device__ void destroy_bodies() {
+    __device__ __forceinline__ void destroy_bodies() {
         if (!S.haveBodies) return;
         S.cHead = NULLN; S.cFree = 0; S.cCount = 0;
         for (int c = 0; c < D::CMAX; ++c) S.cnext[c] = c + 1 < D::CMAX ? c + 1 : NULLN;
@@ -54,7 +54,7 @@ template <int ENV> struct Env : World<ENV> {
         S.haveBodies = 0;
     }
 
-    __device__ void create_dyn_body(int b, float px, float py, float angle) {
+    __device__ __forceinline__ void create_dyn_body(int b, float px, float py, float angle) {
         Rot q = rot(angle);
         S.xpx[b] = px; S.xpy[b] = py; S.xs[b] = q.s; S.xc[b] = q.c;
         V2 c = v2(px, py);
@@ -70,7 +70,7 @@ template <int ENV> struct Env : World<ENV> {
     }
 
     // _generate_blocks / _generate_agents / _generate_boundary (+ v2 _set_random_goal)
-    __device__ void create_bodies(const double* d) {
+    __device__ __forceinline__ void create_bodies(const double* d) {
         int k = 0;
         if (D::V == 0) {
             create_dyn_body(0, (float)d[0], (float)d[1], (float)d[2]);
@@ -98,7 +98,7 @@ template <int ENV> struct Env : World<ENV> {
     }
 
     // _calculate_distance / _calculate_agent_distance
-    __device__ void calc_distances() {
+    __device__ __forceinline__ void calc_distances() {
         if (D::V == 0) {
             for (int b = 0; b < NB; ++b) {
                 float sx = S.cx[b] * 30.0f, sy = S.cy[b] * 30.0f;   // b2Vec2 * SCALE (float32)
@@ -118,18 +118,18 @@ template <int ENV> struct Env : World<ENV> {
         }
     }
 
-    __device__ void unit_vector(int a, int b, double& ux, double& uy) const {   // unitVector :134-138
+    __device__ __forceinline__ void unit_vector(int a, int b, double& ux, double& uy) const {   // unitVector :134-138
         double Ax = S.cx[a], Ay = S.cy[a], Bx = S.cx[b], By = S.cy[b];
         double dx = fabs(Bx - Ax), dy = fabs(By - Ay);
         double denom = dy > dx ? dy : dx;
         ux = (Bx - Ax) / denom; uy = (By - Ay) / denom;
     }
-    __device__ void apply_force(int b, V2 f, V2 point) {   // b2Body::ApplyForce
+    __device__ __forceinline__ void apply_force(int b, V2 f, V2 point) {   // b2Body::ApplyForce
         S.fx[b] = S.fx[b] + f.x; S.fy[b] = S.fy[b] + f.y;
         S.tq[b] += vcross(vsub(point, v2(S.cx[b], S.cy[b])), f);
     }
 
-    __device__ void apply_actions(const float* act) {
+    __device__ __forceinline__ void apply_actions(const float* act) {
         if (D::V == 0) {   // multi_robot_puzzle_00.py:415-424
             const double SPEED = 10.0 / 30.0 * 4;
             for (int i = 0; i < NA; ++i) {
@@ -177,7 +177,7 @@ template <int ENV> struct Env : World<ENV> {
     }
 
     // observation :442-472 / _02.py:494-532, reward + done :475-521 / _02.py:535-584
-    __device__ void obs_reward(const double* prevA, const double* prevB, float* obs, double& reward_out, int& done_out, int& kind_out) {
+    __device__ __forceinline__ void obs_reward(const double* prevA, const double* prevB, float* obs, double& reward_out, int& done_out, int& kind_out) {
         int k = 0;
         bool in_place[NB];
         double reward = 0.0; int done = 0, kind = 0;
@@ -283,9 +283,10 @@ template <int ENV> struct Env : World<ENV> {
 
     // one env step (cooperative: every thread of the wave calls it); reads sh.act, writes
     // sh.obs / sh.reward / sh.done / sh.kind
-    __device__ void env_step_coop() {
+    __device__ __forceinline__ void env_step_coop() {
         if (tid == 0) apply_actions(sh.act);
         __syncthreads();
+        MRP_STAMP(1);
         this->world_step_coop();
         if (tid == 0) {
             double prevA[NA], prevB[NB];
@@ -295,10 +296,11 @@ template <int ENV> struct Env : World<ENV> {
             obs_reward(prevA, prevB, sh.obs, sh.reward, sh.done, sh.kind);
         }
         __syncthreads();
+        MRP_STAMP(7);
     }
 
     // reset(): destroy + rebuild from sh.draws, then the reference's step with sh.act
-    __device__ void env_reset_coop() {
+    __device__ __forceinline__ void env_reset_coop() {
         if (tid == 0) {
             destroy_bodies();
             create_bodies(sh.draws);

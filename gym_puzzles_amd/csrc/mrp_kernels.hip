@@ -84,7 +84,7 @@ __device__ void stage_reset_inputs(Shared<ENV>& sh, const double* draws, const f
 }
 
 template <int ENV>
-__global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* state, int nl, const uint8_t* mask, const double* draws,
+__global__ __launch_bounds__(BLOCK, 4) void k_reset(uint32_t* state, int nl, const uint8_t* mask, const double* draws,
                                                  const float* actions, float* obs, EnvParams P, uint64_t seed,
                                                  uint64_t lane_offset) {
     using D = Dims<ENV>;
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* state, int nl, const 
 }
 
 template <int ENV>
-__global__ __launch_bounds__(BLOCK) void k_step(uint32_t* state, int nl, const float* actions, float* obs, float* reward,
+__global__ __launch_bounds__(BLOCK, 4) void k_step(uint32_t* state, int nl, const float* actions, float* obs, float* reward,
                                                 uint8_t* done_out, uint8_t* trunc_out, uint8_t* status_out, float* term_obs,
                                                 EnvParams P, uint64_t seed, uint64_t lane_offset, int auto_reset,
                                                 int max_steps) {
@@ -112,8 +112,12 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* state, int nl, const f
     const int lane = blockIdx.x, tid = threadIdx.x;
     if (lane >= nl) return;
     const uint64_t glane = lane_offset + lane;
+#ifdef MRP_STAMPS
+    if (tid == 0) sh.stamp_t = __builtin_amdgcn_s_memtime();
+#endif
     load_state<ENV>(sh.S, state, lane, tid);
     __syncthreads();
+    MRP_STAMP(0);
     const uint64_t ctr = (uint64_t)sh.S.stepCounter * 64u;
     if (tid < D::ACT)
         sh.act[tid] = actions ? actions[(size_t)lane * D::ACT + tid] : (float)(-1.0 + 2.0 * rng_u01(seed, glane, 3, ctr + tid));
@@ -135,12 +139,15 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* state, int nl, const f
     float* orow = obs + (size_t)lane * D::OBS;
     if (term_obs)
         for (int k = tid; k < D::OBS; k += BLOCK) term_obs[(size_t)lane * D::OBS + k] = sh.obs[k];
+    MRP_STAMP(8);
     if (s_fin && auto_reset) {   // SB3-style auto-reset with device-RNG spawns
         stage_reset_inputs<ENV>(sh, nullptr, nullptr, lane, tid, seed, glane);
         e.env_reset_coop();
+        MRP_STAMP(9);
     }
     for (int k = tid; k < D::OBS; k += BLOCK) orow[k] = sh.obs[k];
     store_state<ENV>(sh.S, state, lane, tid);
+    MRP_STAMP(10);
 }
 
 __global__ __launch_bounds__(256) void k_sincos(const float* x, float* s, float* c, int n) {
@@ -501,6 +508,21 @@ int mrp_counters(mrp_ctx* ctx, int64_t* toi_events, int64_t* pos_iters) {
     if (toi_events) *toi_events = toi;
     if (pos_iters) *pos_iters = pos;
     return MRP_OK;
+}
+
+// Diagnostic builds only (-DMRP_STAMPS): per-phase thread-0 cycle totals since the last call.
+int mrp_debug_stamps(int device, uint64_t* out16) {
+#ifdef MRP_STAMPS
+    if (!out16 || hipSetDevice(device) != hipSuccess) return MRP_E_HIP;
+    if (hipDeviceSynchronize() != hipSuccess) return MRP_E_HIP;
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamps), 16 * sizeof(uint64_t)) != hipSuccess) return MRP_E_HIP;
+    uint64_t z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) != hipSuccess) return MRP_E_HIP;
+    return MRP_OK;
+#else
+    (void)device; (void)out16;
+    return MRP_E_STATE;
+#endif
 }
 
 int mrp_selftest_sincos(int device, const float* x, float* sin_out, float* cos_out, int n) {

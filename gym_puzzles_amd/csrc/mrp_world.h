@@ -23,6 +23,22 @@
 namespace mrp {
 
 constexpr int NULLN = -1;
+
+// Diagnostic phase timing (build with -DMRP_STAMPS; never in the shipped build): thread 0 of
+// every lane accumulates s_memtime deltas per phase into g_stamps.
+#ifdef MRP_STAMPS
+__device__ unsigned long long g_stamps[16];
+#define MRP_STAMP(k)                                                                        \
+    do {                                                                                    \
+        if (tid == 0) {                                                                     \
+            unsigned long long _t = __builtin_amdgcn_s_memtime();                           \
+            atomicAdd(&g_stamps[k], _t - sh.stamp_t);                                       \
+            sh.stamp_t = _t;                                                                \
+        }                                                                                   \
+    } while (0)
+#else
+#define MRP_STAMP(k) do {} while (0)
+#endif
 constexpr float LINEAR_SLOP = 0.005f;
 constexpr float AABB_EXT = 0.1f;
 constexpr float AABB_MUL = 2.0f;
@@ -117,39 +133,48 @@ template <int ENV> struct Shared {
     using LS = LaneState<ENV>;
     static constexpr int ND = LS::ND, NBODY = ND + 4, C = D::CMAX;
     LS S;
-    VC vcs[C];
-    PC pcs[C];
     IslT<NBODY, C> isl;
     int stack[NBODY];
     float salpha0[4];
-    // collide: contact list snapshot + narrow-phase results (index C is the serial slot)
+    // collide: contact list snapshot (the per-contact manifolds live in the phase union below)
     int clist[C];
     int ccount;
     uint8_t cover[C];
-    int tpc[C + 1], ttype[C + 1];
-    float tlnx[C + 1], tlny[C + 1], tlpx[C + 1], tlpy[C + 1];
-    float tpx[2][C + 1], tpy[2][C + 1];
-    uint32_t tmid[2][C + 1];
-    // broad phase: active proxy ids (ascending) and per-pair overlap flags
+    // serial manifold slot (contact_update outside the parallel narrow phase)
+    int spc, stype;
+    float slnx, slny, slpx, slpy, spx[2], spy[2];
+    uint32_t smid[2];
+    // broad phase: active proxy ids (ascending)
     int nprox;
     uint32_t moved;
     int prox[TREE_N];
-    uint8_t pover[TREE_N * (TREE_N - 1) / 2];
-    // TOI: candidates of one scan (list order) with their post-alpha0-sync sweeps
-    int tn;
+    // TOI scan bookkeeping
+    int tn, np, toi_done, toi_fnc;
     int tcand[C];
-    SweepV tsA[C], tsB[C];
-    TOIOut tout[C];
-    int plan[C];          // per list position: -1 skip, -2 cached, >=0 candidate index
+    int plan[C];          // per list position: -2 cached, >= 0 candidate index
     int pslot[C];
-    int np;
-    int toi_done, toi_fnc;
-    // env outputs
+    // Phase-exclusive scratch (one member live at a time): island solver constraints,
+    // narrow-phase manifolds, pair-overlap flags, TOI candidate sweeps/results.  Each is
+    // consumed before the next phase writes another, which keeps a v0 lane in < 10 KB of LDS
+    // (16 worlds per CU).
+    union U {
+        struct { VC vcs[C]; PC pcs[C]; } sol;
+        struct {
+            int tpc[C], ttype[C];
+            float tlnx[C], tlny[C], tlpx[C], tlpy[C];
+            float tpx[2][C], tpy[2][C];
+            uint32_t tmid[2][C];
+        } col;
+        uint8_t pover[TREE_N * (TREE_N - 1) / 2];
+        struct { SweepV tsA[C], tsB[C]; TOIOut tout[C]; } toi;
+    } u;
+    // env I/O
     float obs[D::OBS];
     double reward;
     int done, kind;
     float act[D::ACT];
     double draws[D::NDRAW];
+    unsigned long long stamp_t;
 };
 
 template <int ENV> struct World {
@@ -165,19 +190,19 @@ template <int ENV> struct World {
     const EnvParams& P;
     const int tid;
 
-    __device__ World(SH& s, const EnvTables& t, const EnvParams& p, int thread) : sh(s), S(s.S), T(t), P(p), tid(thread) {}
+    __device__ __forceinline__ World(SH& s, const EnvTables& t, const EnvParams& p, int thread) : sh(s), S(s.S), T(t), P(p), tid(thread) {}
 
     // ------------------------------------------------------------------ bodies
-    __device__ bool is_dyn(int b) const { return b < ND; }
-    __device__ Xf xf(int b) const {
+    __device__ __forceinline__ bool is_dyn(int b) const { return b < ND; }
+    __device__ __forceinline__ Xf xf(int b) const {
         Xf r;
         if (b < ND) { r.p = v2(S.xpx[b], S.xpy[b]); r.q.s = S.xs[b]; r.q.c = S.xc[b]; }
         else { r.p = v2(T.wall_px[b - ND], T.wall_py[b - ND]); r.q.s = 0.0f; r.q.c = 1.0f; }
         return r;
     }
-    __device__ V2 center(int b) const { return b < ND ? v2(S.cx[b], S.cy[b]) : v2(T.wall_px[b - ND], T.wall_py[b - ND]); }
-    __device__ V2 lc(int b) const { return v2(T.lcx[b], T.lcy[b]); }
-    __device__ void sync_transform(int b) {   // b2Body::SynchronizeTransform
+    __device__ __forceinline__ V2 center(int b) const { return b < ND ? v2(S.cx[b], S.cy[b]) : v2(T.wall_px[b - ND], T.wall_py[b - ND]); }
+    __device__ __forceinline__ V2 lc(int b) const { return v2(T.lcx[b], T.lcy[b]); }
+    __device__ __forceinline__ void sync_transform(int b) {   // b2Body::SynchronizeTransform
         Rot q = rot(S.a[b]);
         S.xs[b] = q.s; S.xc[b] = q.c;
         V2 p = vsub(v2(S.cx[b], S.cy[b]), mul_rv(q, lc(b)));
@@ -185,21 +210,21 @@ template <int ENV> struct World {
     }
 
     // ------------------------------------------------------------------ dynamic tree
-    __device__ static float perim(float lx, float ly, float hx, float hy) { float wx = hx - lx; float wy = hy - ly; return 2.0f * (wx + wy); }
-    __device__ int t_alloc() {
+    __device__ __forceinline__ static float perim(float lx, float ly, float hx, float hy) { float wx = hx - lx; float wy = hy - ly; return 2.0f * (wx + wy); }
+    __device__ __forceinline__ int t_alloc() {
         int id = S.freeList;
         S.freeList = S.tpar[id];
         S.tpar[id] = NULLN; S.tc1[id] = NULLN; S.tc2[id] = NULLN; S.th[id] = 0; S.tud[id] = -1;
         ++S.nodeCount;
         return id;
     }
-    __device__ void t_free(int id) { S.tpar[id] = S.freeList; S.th[id] = -1; S.tud[id] = -1; S.freeList = id; --S.nodeCount; }
-    __device__ bool t_leaf(int id) const { return S.tc1[id] == NULLN; }
-    __device__ void t_combine_into(int dst, int a, int b) {
+    __device__ __forceinline__ void t_free(int id) { S.tpar[id] = S.freeList; S.th[id] = -1; S.tud[id] = -1; S.freeList = id; --S.nodeCount; }
+    __device__ __forceinline__ bool t_leaf(int id) const { return S.tc1[id] == NULLN; }
+    __device__ __forceinline__ void t_combine_into(int dst, int a, int b) {
         S.tlx[dst] = fmin_(S.tlx[a], S.tlx[b]); S.tly[dst] = fmin_(S.tly[a], S.tly[b]);
         S.thx[dst] = fmax_(S.thx[a], S.thx[b]); S.thy[dst] = fmax_(S.thy[a], S.thy[b]);
     }
-    __device__ int t_balance(int iA) {
+    __device__ __forceinline__ int t_balance(int iA) {
         if (t_leaf(iA) || S.th[iA] < 2) return iA;
         int iB = S.tc1[iA], iC = S.tc2[iA];
         int balance = S.th[iC] - S.th[iB];
@@ -239,7 +264,7 @@ template <int ENV> struct World {
         }
         return iA;
     }
-    __device__ void t_fix_upwards(int index) {
+    __device__ __forceinline__ void t_fix_upwards(int index) {
         while (index != NULLN) {
             index = t_balance(index);
             int c1 = S.tc1[index], c2 = S.tc2[index];
@@ -248,7 +273,7 @@ template <int ENV> struct World {
             index = S.tpar[index];
         }
     }
-    __device__ void t_insert(int leaf) {
+    __device__ __forceinline__ void t_insert(int leaf) {
         if (S.root == NULLN) { S.root = leaf; S.tpar[leaf] = NULLN; return; }
         float llx = S.tlx[leaf], lly = S.tly[leaf], lhx = S.thx[leaf], lhy = S.thy[leaf];
         int index = S.root;
@@ -284,7 +309,7 @@ template <int ENV> struct World {
         S.tc1[np] = sibling; S.tc2[np] = leaf; S.tpar[sibling] = np; S.tpar[leaf] = np;
         t_fix_upwards(S.tpar[leaf]);
     }
-    __device__ void t_remove(int leaf) {
+    __device__ __forceinline__ void t_remove(int leaf) {
         if (leaf == S.root) { S.root = NULLN; return; }
         int parent = S.tpar[leaf];
         int grand = S.tpar[parent];
@@ -305,16 +330,16 @@ template <int ENV> struct World {
             S.root = sibling; S.tpar[sibling] = NULLN; t_free(parent);
         }
     }
-    __device__ void buffer_move(int id) { S.moveBuf[S.moveCount++] = id; }
-    __device__ void unbuffer_move(int id) { for (int i = 0; i < S.moveCount; ++i) if (S.moveBuf[i] == id) S.moveBuf[i] = NULLN; }
+    __device__ __forceinline__ void buffer_move(int id) { S.moveBuf[S.moveCount++] = id; }
+    __device__ __forceinline__ void unbuffer_move(int id) { for (int i = 0; i < S.moveCount; ++i) if (S.moveBuf[i] == id) S.moveBuf[i] = NULLN; }
 
     // polygon AABB under a transform (b2PolygonShape::ComputeAABB)
-    __device__ void poly_aabb(const ShapeDef& s, Xf x, float& lx, float& ly, float& hx, float& hy) const {
+    __device__ __forceinline__ void poly_aabb(const ShapeDef& s, Xf x, float& lx, float& ly, float& hx, float& hy) const {
         V2 lower = mul_xv(x, s.v[0]), upper = lower;
         for (int i = 1; i < s.count; ++i) { V2 v = mul_xv(x, s.v[i]); lower = vmin(lower, v); upper = vmax(upper, v); }
         lx = lower.x - s.radius; ly = lower.y - s.radius; hx = upper.x + s.radius; hy = upper.y + s.radius;
     }
-    __device__ void create_proxy(int f, Xf x) {
+    __device__ __forceinline__ void create_proxy(int f, Xf x) {
         float lx, ly, hx, hy;
         poly_aabb(T.shape[f], x, lx, ly, hx, hy);
         int id = t_alloc();
@@ -324,12 +349,12 @@ template <int ENV> struct World {
         S.proxy[f] = id;
         buffer_move(id);
     }
-    __device__ void destroy_proxy(int f) {
+    __device__ __forceinline__ void destroy_proxy(int f) {
         int id = S.proxy[f];
         unbuffer_move(id);
         t_remove(id); t_free(id);
     }
-    __device__ void move_proxy(int id, float lx, float ly, float hx, float hy, V2 disp) {
+    __device__ __forceinline__ void move_proxy(int id, float lx, float ly, float hx, float hy, V2 disp) {
         if (S.tlx[id] <= lx && S.tly[id] <= ly && hx <= S.thx[id] && hy <= S.thy[id]) return;   // Contains
         t_remove(id);
         float blx = lx - AABB_EXT, bly = ly - AABB_EXT, bhx = hx + AABB_EXT, bhy = hy + AABB_EXT;
@@ -340,7 +365,7 @@ template <int ENV> struct World {
         t_insert(id);
         buffer_move(id);
     }
-    __device__ bool fat_overlap(int a, int b) const {   // b2TestOverlap
+    __device__ __forceinline__ bool fat_overlap(int a, int b) const {   // b2TestOverlap
         float d1x = S.tlx[b] - S.thx[a], d1y = S.tly[b] - S.thy[a];
         float d2x = S.tlx[a] - S.thx[b], d2y = S.tly[a] - S.thy[b];
         if (d1x > 0.0f || d1y > 0.0f) return false;
@@ -348,7 +373,7 @@ template <int ENV> struct World {
         return true;
     }
     // b2Body::SynchronizeFixtures for a dynamic body, fixtures in fixture-list order (newest first)
-    __device__ void sync_fixtures(int b) {
+    __device__ __forceinline__ void sync_fixtures(int b) {
         Xf x1; x1.q = rot(S.a0[b]);
         x1.p = vsub(v2(S.c0x[b], S.c0y[b]), mul_rv(x1.q, lc(b)));
         Xf x2 = xf(b);
@@ -363,7 +388,7 @@ template <int ENV> struct World {
     }
 
     // ------------------------------------------------------------------ contacts
-    __device__ void contact_event(int c, int value) {   // ContactDetector (multi_robot_puzzle_00.py:92-111)
+    __device__ __forceinline__ void contact_event(int c, int value) {   // ContactDetector (multi_robot_puzzle_00.py:92-111)
         int bA = T.fix_body[S.cfa[c]], bB = T.fix_body[S.cfb[c]];
         for (int i = 0; i < NA; ++i) {
             int ag = NB + i;
@@ -373,7 +398,7 @@ template <int ENV> struct World {
             }
         }
     }
-    __device__ void add_pair(int fa, int fb) {   // b2ContactManager::AddPair
+    __device__ __forceinline__ void add_pair(int fa, int fb) {   // b2ContactManager::AddPair
         int bA = T.fix_body[fa], bB = T.fix_body[fb];
         if (bA == bB) return;
         for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
@@ -390,7 +415,7 @@ template <int ENV> struct World {
         S.cHead = c;
         ++S.cCount;
     }
-    __device__ void destroy_contact(int c, bool events) {   // b2ContactManager::Destroy
+    __device__ __forceinline__ void destroy_contact(int c, bool events) {   // b2ContactManager::Destroy
         if (events && (S.cflags[c] & CF_TOUCHING)) contact_event(c, 0);
         int p = S.cprev[c], n = S.cnext[c];
         if (p != NULLN) S.cnext[p] = n;
@@ -403,7 +428,7 @@ template <int ENV> struct World {
     // moved proxy and overlapping fat AABBs, visited in sorted order == Box2D's sorted pair buffer.
     // Cooperative: every thread of the wave calls it; the O(P^2) overlap tests run in parallel,
     // the order-sensitive AddPair calls run on thread 0 in sorted order.
-    __device__ void find_new_contacts_coop() {
+    __device__ __forceinline__ void find_new_contacts_coop() {
         if (tid == 0) {
             uint32_t moved = 0;
             for (int i = 0; i < S.moveCount; ++i) if (S.moveBuf[i] != NULLN) moved |= 1u << S.moveBuf[i];
@@ -422,23 +447,23 @@ template <int ENV> struct World {
             int i = 0, q = p;
             while (q >= n - 1 - i) { q -= n - 1 - i; ++i; }
             int a = sh.prox[i], b = sh.prox[i + 1 + q];
-            sh.pover[p] = ((((moved >> a) | (moved >> b)) & 1u) && fat_overlap(a, b)) ? 1 : 0;
+            sh.u.pover[p] = ((((moved >> a) | (moved >> b)) & 1u) && fat_overlap(a, b)) ? 1 : 0;
         }
         __syncthreads();
         if (tid == 0) {
             int p = 0;
             for (int i = 0; i < n; ++i)
                 for (int j = i + 1; j < n; ++j, ++p)
-                    if (sh.pover[p]) add_pair(S.tud[sh.prox[i]], S.tud[sh.prox[j]]);
+                    if (sh.u.pover[p]) add_pair(S.tud[sh.prox[i]], S.tud[sh.prox[j]]);
         }
         __syncthreads();
     }
 
     // ---------------------------------------------------------------- narrow phase (b2CollidePolygons)
-    __device__ static uint32_t cf_make(int iA, int iB, int tA, int tB) {
+    __device__ __forceinline__ static uint32_t cf_make(int iA, int iB, int tA, int tB) {
         return (uint32_t)(uint8_t)iA | ((uint32_t)(uint8_t)iB << 8) | ((uint32_t)(uint8_t)tA << 16) | ((uint32_t)(uint8_t)tB << 24);
     }
-    __device__ static float find_max_separation(int& edge, const ShapeDef& p1, Xf x1, const ShapeDef& p2, Xf x2) {
+    __device__ __forceinline__ static float find_max_separation(int& edge, const ShapeDef& p1, Xf x1, const ShapeDef& p2, Xf x2) {
         Xf x = mulT_xx(x2, x1);
         int best = 0; float maxSep = -FLT_MAXV;
         for (int i = 0; i < p1.count; ++i) {
@@ -452,7 +477,7 @@ template <int ENV> struct World {
         return maxSep;
     }
     // b2ClipSegmentToLine with the two in/out vertices kept in registers
-    __device__ static int clip(ClipV& o0, ClipV& o1, const ClipV& i0, const ClipV& i1, V2 normal, float offset, int vertexIndexA) {
+    __device__ __forceinline__ static int clip(ClipV& o0, ClipV& o1, const ClipV& i0, const ClipV& i1, V2 normal, float offset, int vertexIndexA) {
         int numOut = 0;
         float d0 = vdot(normal, i0.v) - offset;
         float d1 = vdot(normal, i1.v) - offset;
@@ -466,9 +491,19 @@ template <int ENV> struct World {
         }
         return numOut;
     }
-    // b2CollidePolygons into manifold scratch slot k (sh.t*[k])
-    __device__ void collide_polygons(int k, const ShapeDef& pA, Xf xA, const ShapeDef& pB, Xf xB) {
-        sh.tpc[k] = 0;
+    // manifold scratch: parallel slot k (narrow phase) or the serial slot (k < 0)
+    __device__ __forceinline__ int& m_pc(int k) { return k < 0 ? sh.spc : sh.u.col.tpc[k]; }
+    __device__ __forceinline__ int& m_type(int k) { return k < 0 ? sh.stype : sh.u.col.ttype[k]; }
+    __device__ __forceinline__ float& m_lnx(int k) { return k < 0 ? sh.slnx : sh.u.col.tlnx[k]; }
+    __device__ __forceinline__ float& m_lny(int k) { return k < 0 ? sh.slny : sh.u.col.tlny[k]; }
+    __device__ __forceinline__ float& m_lpx(int k) { return k < 0 ? sh.slpx : sh.u.col.tlpx[k]; }
+    __device__ __forceinline__ float& m_lpy(int k) { return k < 0 ? sh.slpy : sh.u.col.tlpy[k]; }
+    __device__ __forceinline__ float& m_px(int i, int k) { return k < 0 ? sh.spx[i] : sh.u.col.tpx[i][k]; }
+    __device__ __forceinline__ float& m_py(int i, int k) { return k < 0 ? sh.spy[i] : sh.u.col.tpy[i][k]; }
+    __device__ __forceinline__ uint32_t& m_id(int i, int k) { return k < 0 ? sh.smid[i] : sh.u.col.tmid[i][k]; }
+    // b2CollidePolygons into manifold scratch slot k
+    __device__ __forceinline__ void collide_polygons(int k, const ShapeDef& pA, Xf xA, const ShapeDef& pB, Xf xB) {
+        m_pc(k) = 0;
         float totalRadius = pA.radius + pB.radius;
         int edgeA = 0;
         float sepA = find_max_separation(edgeA, pA, xA, pB, xB);
@@ -482,7 +517,7 @@ template <int ENV> struct World {
         const ShapeDef& p2 = flip ? pA : pB;
         Xf x1 = flip ? xB : xA, x2 = flip ? xA : xB;
         int edge1 = flip ? edgeB : edgeA;
-        sh.ttype[k] = flip ? MT_FACEB : MT_FACEA;
+        m_type(k) = flip ? MT_FACEB : MT_FACEA;
         ClipV inc0, inc1;   // incident edge
         {
             V2 normal1 = mulT_rv(x2.q, mul_rv(x1.q, p1.n[edge1]));
@@ -507,8 +542,8 @@ template <int ENV> struct World {
         ClipV a0, a1, b0, b1;
         if (clip(a0, a1, inc0, inc1, vneg(tangent), side1, iv1) < 2) return;
         if (clip(b0, b1, a0, a1, tangent, side2, iv2) < 2) return;
-        sh.tlnx[k] = localNormal.x; sh.tlny[k] = localNormal.y;
-        sh.tlpx[k] = planePoint.x; sh.tlpy[k] = planePoint.y;
+        m_lnx(k) = localNormal.x; m_lny(k) = localNormal.y;
+        m_lpx(k) = planePoint.x; m_lpy(k) = planePoint.y;
         int pc = 0;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -521,30 +556,30 @@ template <int ENV> struct World {
                     uint32_t q0 = id & 0xff, q1 = (id >> 8) & 0xff, ta = (id >> 16) & 0xff, tb = (id >> 24) & 0xff;
                     id = q1 | (q0 << 8) | (tb << 16) | (ta << 24);
                 }
-                if (pc == 0) { sh.tpx[0][k] = lp.x; sh.tpy[0][k] = lp.y; sh.tmid[0][k] = id; }
-                else { sh.tpx[1][k] = lp.x; sh.tpy[1][k] = lp.y; sh.tmid[1][k] = id; }
+                if (pc == 0) { m_px(0, k) = lp.x; m_py(0, k) = lp.y; m_id(0, k) = id; }
+                else { m_px(1, k) = lp.x; m_py(1, k) = lp.y; m_id(1, k) = id; }
                 ++pc;
             }
         }
-        sh.tpc[k] = pc;
+        m_pc(k) = pc;
     }
     // second half of b2Contact::Update: adopt manifold scratch slot k, match feature ids to
     // carry the warm-start impulses, update the touching flag, fire Begin/End events
-    __device__ void contact_commit(int c, int k) {
+    __device__ __forceinline__ void contact_commit(int c, int k) {
         int oldCount = S.mpc[c];
         uint32_t oid0 = S.mid[0][c], oid1 = S.mid[1][c];
         float on0 = S.mni[0][c], on1 = S.mni[1][c], ot0 = S.mti[0][c], ot1 = S.mti[1][c];
         S.cflags[c] |= CF_ENABLED;
         bool wasTouching = (S.cflags[c] & CF_TOUCHING) != 0;
-        int pcount = sh.tpc[k];
+        int pcount = m_pc(k);
         S.mpc[c] = pcount;
         if (pcount > 0) {
-            S.mtype[c] = sh.ttype[k];
-            S.mlnx[c] = sh.tlnx[k]; S.mlny[c] = sh.tlny[k]; S.mlpx[c] = sh.tlpx[k]; S.mlpy[c] = sh.tlpy[k];
+            S.mtype[c] = m_type(k);
+            S.mlnx[c] = m_lnx(k); S.mlny[c] = m_lny(k); S.mlpx[c] = m_lpx(k); S.mlpy[c] = m_lpy(k);
         }
         for (int i = 0; i < pcount; ++i) {
-            uint32_t id2 = sh.tmid[i][k];
-            S.mpx[i][c] = sh.tpx[i][k]; S.mpy[i][c] = sh.tpy[i][k]; S.mid[i][c] = id2;
+            uint32_t id2 = m_id(i, k);
+            S.mpx[i][c] = m_px(i, k); S.mpy[i][c] = m_py(i, k); S.mid[i][c] = id2;
             float ni = 0.0f, ti = 0.0f;
             if (oldCount > 0 && oid0 == id2) { ni = on0; ti = ot0; }
             else if (oldCount > 1 && oid1 == id2) { ni = on1; ti = ot1; }
@@ -556,15 +591,15 @@ template <int ENV> struct World {
         if (wasTouching && !touching) contact_event(c, 0);
     }
     // b2Contact::Update on one contact (serial callers: TOI)
-    __device__ void contact_update(int c) {
+    __device__ __forceinline__ void contact_update(int c) {
         int fa = S.cfa[c], fb = S.cfb[c];
-        collide_polygons(C, T.shape[fa], xf(T.fix_body[fa]), T.shape[fb], xf(T.fix_body[fb]));
-        contact_commit(c, C);
+        collide_polygons(-1, T.shape[fa], xf(T.fix_body[fa]), T.shape[fb], xf(T.fix_body[fb]));
+        contact_commit(c, -1);
     }
     // b2ContactManager::Collide.  Cooperative: thread 0 snapshots the contact list, all threads
     // run the broad-phase overlap test + SAT narrow phase of one contact each, then thread 0
     // destroys / commits in list order (events fire in the reference's order).
-    __device__ void collide_coop() {
+    __device__ __forceinline__ void collide_coop() {
         if (tid == 0) {
             int n = 0;
             for (int c = S.cHead; c != NULLN; c = S.cnext[c]) sh.clist[n++] = c;
@@ -591,10 +626,10 @@ template <int ENV> struct World {
     }
 
     // ---------------------------------------------------------------- contact solver
-    __device__ float body_invMass(int b) const { return T.invMass[b]; }
-    __device__ float body_invI(int b) const { return T.invI[b]; }
+    __device__ __forceinline__ float body_invMass(int b) const { return T.invMass[b]; }
+    __device__ __forceinline__ float body_invI(int b) const { return T.invI[b]; }
 
-    __device__ void solver_init(Isl& is, VC* vcs, PC* pcs, bool warm, float dtRatio) {
+    __device__ __forceinline__ void solver_init(Isl& is, VC* vcs, PC* pcs, bool warm, float dtRatio) {
         for (int i = 0; i < is.nc; ++i) {
             int c = is.contacts[i];
             int fa = S.cfa[c], fb = S.cfb[c];
@@ -621,7 +656,7 @@ template <int ENV> struct World {
             }
         }
     }
-    __device__ void solver_init_velocity(Isl& is, VC* vcs, PC* pcs) {
+    __device__ __forceinline__ void solver_init_velocity(Isl& is, VC* vcs, PC* pcs) {
         for (int i = 0; i < is.nc; ++i) {
             VC& vc = vcs[i]; PC& pc = pcs[i];
             int c = vc.slot;
@@ -693,7 +728,7 @@ template <int ENV> struct World {
             }
         }
     }
-    __device__ void solver_warm_start(Isl& is, VC* vcs) {
+    __device__ __forceinline__ void solver_warm_start(Isl& is, VC* vcs) {
         for (int i = 0; i < is.nc; ++i) {
             VC& vc = vcs[i];
             int ia = vc.iaI, ib = vc.ibI;
@@ -711,7 +746,7 @@ template <int ENV> struct World {
             is.vvx[ib] = vB.x; is.vvy[ib] = vB.y; is.vw[ib] = wB;
         }
     }
-    __device__ void solver_velocity(Isl& is, VC* vcs) {   // b2ContactSolver::SolveVelocityConstraints
+    __device__ __forceinline__ void solver_velocity(Isl& is, VC* vcs) {   // b2ContactSolver::SolveVelocityConstraints
         for (int i = 0; i < is.nc; ++i) {
             VC& vc = vcs[i];
             int ia = vc.iaI, ib = vc.ibI;
@@ -789,13 +824,13 @@ template <int ENV> struct World {
             is.vvx[ib] = vB.x; is.vvy[ib] = vB.y; is.vw[ib] = wB;
         }
     }
-    __device__ void solver_store(Isl& is, VC* vcs) {
+    __device__ __forceinline__ void solver_store(Isl& is, VC* vcs) {
         for (int i = 0; i < is.nc; ++i) {
             VC& vc = vcs[i];
             for (int j = 0; j < vc.pointCount; ++j) { S.mni[j][vc.slot] = vc.ni[j]; S.mti[j][vc.slot] = vc.ti[j]; }
         }
     }
-    __device__ bool solver_position(Isl& is, PC* pcs, bool toi, int toiA, int toiB) {
+    __device__ __forceinline__ bool solver_position(Isl& is, PC* pcs, bool toi, int toiA, int toiB) {
         float minSep = 0.0f;
         for (int i = 0; i < is.nc; ++i) {
             PC& pc = pcs[i];
@@ -845,7 +880,7 @@ template <int ENV> struct World {
         }
         return toi ? (minSep >= -1.5f * LINEAR_SLOP) : (minSep >= -3.0f * LINEAR_SLOP);
     }
-    __device__ void integrate_positions(Isl& is, float h) {
+    __device__ __forceinline__ void integrate_positions(Isl& is, float h) {
         for (int i = 0; i < is.nb; ++i) {
             V2 c = v2(is.pcx[i], is.pcy[i]); float a = is.pa[i];
             V2 v = v2(is.vvx[i], is.vvy[i]); float w = is.vw[i];
@@ -865,10 +900,10 @@ template <int ENV> struct World {
             is.vvx[i] = v.x; is.vvy[i] = v.y; is.vw[i] = w;
         }
     }
-    __device__ void island_add_body(Isl& is, int b) { is.index[b] = is.nb; is.bodies[is.nb++] = b; }
+    __device__ __forceinline__ void island_add_body(Isl& is, int b) { is.index[b] = is.nb; is.bodies[is.nb++] = b; }
 
     // b2Island::Solve (discrete step of one island)
-    __device__ void island_solve(Isl& is, float h, float dtRatio, VC* vcs, PC* pcs) {
+    __device__ __forceinline__ void island_solve(Isl& is, float h, float dtRatio, VC* vcs, PC* pcs) {
         for (int i = 0; i < is.nb; ++i) {
             int b = is.bodies[i];
             if (is_dyn(b)) {
@@ -887,15 +922,21 @@ template <int ENV> struct World {
                 is.pcx[i] = c.x; is.pcy[i] = c.y; is.pa[i] = 0.0f; is.vvx[i] = 0.0f; is.vvy[i] = 0.0f; is.vw[i] = 0.0f;
             }
         }
-        solver_init(is, vcs, pcs, true, dtRatio);
-        solver_init_velocity(is, vcs, pcs);
-        solver_warm_start(is, vcs);
-        for (int it = 0; it < 180; ++it) solver_velocity(is, vcs);
-        solver_store(is, vcs);
+        if (is.nc > 0) {
+            solver_init(is, vcs, pcs, true, dtRatio);
+            solver_init_velocity(is, vcs, pcs);
+            solver_warm_start(is, vcs);
+            for (int it = 0; it < 180; ++it) solver_velocity(is, vcs);
+            solver_store(is, vcs);
+        }
         integrate_positions(is, h);
-        for (int it = 0; it < 60; ++it) {
-            ++S.posIters;
-            if (solver_position(is, pcs, false, -1, -1)) break;
+        if (is.nc > 0) {
+            for (int it = 0; it < 60; ++it) {
+                ++S.posIters;
+                if (solver_position(is, pcs, false, -1, -1)) break;
+            }
+        } else {
+            ++S.posIters;   // an empty island's first position pass already reports solved
         }
         for (int i = 0; i < is.nb; ++i) {
             int b = is.bodies[i];
@@ -908,7 +949,7 @@ template <int ENV> struct World {
 
     // b2World::Solve, serial part (thread 0): island DFS + island solves + SynchronizeFixtures.
     // The trailing FindNewContacts is cooperative and issued by world_step_coop.
-    __device__ void solve_serial(float h, float dtRatio) {
+    __device__ __forceinline__ void solve_serial(float h, float dtRatio) {
         Isl& is = sh.isl;
         uint32_t bflag = 0;   // body island flags (bit per body)
         for (int c = S.cHead; c != NULLN; c = S.cnext[c]) S.cflags[c] &= ~CF_ISLAND;
@@ -935,20 +976,20 @@ template <int ENV> struct World {
                     stack[sc++] = other; bflag |= 1u << other;
                 }
             }
-            island_solve(is, h, dtRatio, sh.vcs, sh.pcs);
+            island_solve(is, h, dtRatio, sh.u.sol.vcs, sh.u.sol.pcs);
             for (int i = 0; i < is.nb; ++i) if (!is_dyn(is.bodies[i])) bflag &= ~(1u << is.bodies[i]);
         }
         for (int b = ND - 1; b >= 0; --b) if (bflag & (1u << b)) sync_fixtures(b);
     }
 
     // ---------------------------------------------------------------- TOI
-    __device__ SweepV sweep(int b, const float* salpha0) const {
+    __device__ __forceinline__ SweepV sweep(int b, const float* salpha0) const {
         SweepV s;
         if (b < ND) { s.lcx = T.lcx[b]; s.lcy = T.lcy[b]; s.c0x = S.c0x[b]; s.c0y = S.c0y[b]; s.cx = S.cx[b]; s.cy = S.cy[b]; s.a0 = S.a0[b]; s.a = S.a[b]; s.alpha0 = S.alpha0[b]; }
         else { s.lcx = 0.0f; s.lcy = 0.0f; s.c0x = s.cx = T.wall_px[b - ND]; s.c0y = s.cy = T.wall_py[b - ND]; s.a0 = s.a = 0.0f; s.alpha0 = salpha0[b - ND]; }
         return s;
     }
-    __device__ static Xf sweep_xf(const SweepV& s, float beta) {
+    __device__ __forceinline__ static Xf sweep_xf(const SweepV& s, float beta) {
         Xf x;
         x.p = vadd(vmul(1.0f - beta, v2(s.c0x, s.c0y)), vmul(beta, v2(s.cx, s.cy)));
         float angle = (1.0f - beta) * s.a0 + beta * s.a;
@@ -956,18 +997,18 @@ template <int ENV> struct World {
         x.p = vsub(x.p, mul_rv(x.q, v2(s.lcx, s.lcy)));
         return x;
     }
-    __device__ static void sweep_advance(SweepV& s, float alpha) {
+    __device__ __forceinline__ static void sweep_advance(SweepV& s, float alpha) {
         float beta = (alpha - s.alpha0) / (1.0f - s.alpha0);
         V2 c0 = vadd(v2(s.c0x, s.c0y), vmul(beta, vsub(v2(s.cx, s.cy), v2(s.c0x, s.c0y))));
         s.c0x = c0.x; s.c0y = c0.y;
         s.a0 += beta * (s.a - s.a0);
         s.alpha0 = alpha;
     }
-    __device__ void sweep_store(int b, const SweepV& s, float* salpha0) {
+    __device__ __forceinline__ void sweep_store(int b, const SweepV& s, float* salpha0) {
         if (b < ND) { S.c0x[b] = s.c0x; S.c0y[b] = s.c0y; S.cx[b] = s.cx; S.cy[b] = s.cy; S.a0[b] = s.a0; S.a[b] = s.a; S.alpha0[b] = s.alpha0; }
         else salpha0[b - ND] = s.alpha0;
     }
-    __device__ void body_advance(int b, float alpha, float* salpha0) {   // b2Body::Advance
+    __device__ __forceinline__ void body_advance(int b, float alpha, float* salpha0) {   // b2Body::Advance
         SweepV s = sweep(b, salpha0);
         sweep_advance(s, alpha);
         s.cx = s.c0x; s.cy = s.c0y; s.a = s.a0;
@@ -975,17 +1016,17 @@ template <int ENV> struct World {
         if (b < ND) sync_transform(b);
     }
 
-    __device__ static int support(const DProxy& p, V2 d) {
+    __device__ __forceinline__ static int support(const DProxy& p, V2 d) {
         int best = 0; float bv = vdot(p.v[0], d);
         for (int i = 1; i < p.count; ++i) { float val = vdot(p.v[i], d); if (val > bv) { best = i; bv = val; } }
         return best;
     }
-    __device__ static float s_metric(const Simplex& s) {
+    __device__ __forceinline__ static float s_metric(const Simplex& s) {
         if (s.count == 2) return vlen(vsub(s.v[0].w, s.v[1].w));
         if (s.count == 3) return vcross(vsub(s.v[1].w, s.v[0].w), vsub(s.v[2].w, s.v[0].w));
         return 0.0f;
     }
-    __device__ static void s_solve2(Simplex& s) {
+    __device__ __forceinline__ static void s_solve2(Simplex& s) {
         V2 w1 = s.v[0].w, w2 = s.v[1].w, e12 = vsub(w2, w1);
         float d12_2 = -vdot(w1, e12);
         if (d12_2 <= 0.0f) { s.v[0].a = 1.0f; s.count = 1; return; }
@@ -994,7 +1035,7 @@ template <int ENV> struct World {
         float inv = 1.0f / (d12_1 + d12_2);
         s.v[0].a = d12_1 * inv; s.v[1].a = d12_2 * inv; s.count = 2;
     }
-    __device__ static void s_solve3(Simplex& s) {
+    __device__ __forceinline__ static void s_solve3(Simplex& s) {
         V2 w1 = s.v[0].w, w2 = s.v[1].w, w3 = s.v[2].w;
         V2 e12 = vsub(w2, w1);
         float d12_1 = vdot(w2, e12), d12_2 = -vdot(w1, e12);
@@ -1014,7 +1055,7 @@ template <int ENV> struct World {
         s.v[0].a = d123_1 * inv; s.v[1].a = d123_2 * inv; s.v[2].a = d123_3 * inv; s.count = 3;
     }
     // b2Distance (GJK), returns distance between the (radius-free) cores
-    __device__ static float gjk(SCache& cache, const DProxy& pA, Xf xA, const DProxy& pB, Xf xB) {
+    __device__ __forceinline__ static float gjk(SCache& cache, const DProxy& pA, Xf xA, const DProxy& pB, Xf xB) {
         Simplex s;
         s.count = cache.count;
         for (int i = 0; i < s.count; ++i) {
@@ -1073,7 +1114,7 @@ template <int ENV> struct World {
         for (int i = 0; i < s.count; ++i) { cache.iA[i] = s.v[i].iA; cache.iB[i] = s.v[i].iB; }
         return dist;
     }
-    __device__ static float sep_eval(const SepFn& f, const DProxy& pA, const DProxy& pB, const SweepV& sA, const SweepV& sB, int iA, int iB, float t) {
+    __device__ __forceinline__ static float sep_eval(const SepFn& f, const DProxy& pA, const DProxy& pB, const SweepV& sA, const SweepV& sB, int iA, int iB, float t) {
         Xf xA = sweep_xf(sA, t), xB = sweep_xf(sB, t);
         if (f.type == 0) return vdot(vsub(mul_xv(xB, pB.v[iB]), mul_xv(xA, pA.v[iA])), f.axis);
         if (f.type == 1) {
@@ -1085,7 +1126,7 @@ template <int ENV> struct World {
         V2 pointB = mul_xv(xB, f.lp);
         return vdot(vsub(mul_xv(xA, pA.v[iA]), pointB), normal);
     }
-    __device__ static float sep_min(const SepFn& f, const DProxy& pA, const DProxy& pB, const SweepV& sA, const SweepV& sB, int& iA, int& iB, float t) {
+    __device__ __forceinline__ static float sep_min(const SepFn& f, const DProxy& pA, const DProxy& pB, const SweepV& sA, const SweepV& sB, int& iA, int& iB, float t) {
         Xf xA = sweep_xf(sA, t), xB = sweep_xf(sB, t);
         if (f.type == 0) {
             iA = support(pA, mulT_rv(xA.q, f.axis)); iB = support(pB, mulT_rv(xB.q, vneg(f.axis)));
@@ -1103,7 +1144,7 @@ template <int ENV> struct World {
         return vdot(vsub(mul_xv(xA, pA.v[iA]), pointB), normal);
     }
     // b2TimeOfImpact; state 3 == e_touching
-    __device__ static TOIOut time_of_impact(const DProxy& pA, const DProxy& pB, SweepV sA, SweepV sB) {
+    __device__ __forceinline__ static TOIOut time_of_impact(const DProxy& pA, const DProxy& pB, SweepV sA, SweepV sB) {
         TOIOut out; out.state = 0; out.t = 1.0f;
         {   // b2Sweep::Normalize
             float twoPi = 2.0f * B2_PI;
@@ -1185,7 +1226,7 @@ template <int ENV> struct World {
     }
 
     // b2Island::SolveTOI
-    __device__ void island_solve_toi(Isl& is, float dt, int toiA, int toiB, VC* vcs, PC* pcs, const float* salpha0) {
+    __device__ __forceinline__ void island_solve_toi(Isl& is, float dt, int toiA, int toiB, VC* vcs, PC* pcs, const float* salpha0) {
         for (int i = 0; i < is.nb; ++i) {
             int b = is.bodies[i];
             if (is_dyn(b)) { is.pcx[i] = S.cx[b]; is.pcy[i] = S.cy[b]; is.pa[i] = S.a[b]; is.vvx[i] = S.vx[b]; is.vvy[i] = S.vy[b]; is.vw[i] = S.w[b]; }
@@ -1215,7 +1256,7 @@ template <int ENV> struct World {
     // reference's scan does) and snapshotting the sweeps of every contact whose TOI must be
     // computed; all threads then run b2TimeOfImpact on one candidate each; thread 0 takes the
     // minimum in list order and processes the event serially.
-    __device__ void toi_scan() {
+    __device__ __forceinline__ void toi_scan() {
         float* salpha0 = sh.salpha0;
         int tn = 0, np = 0;
         for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
@@ -1229,14 +1270,14 @@ template <int ENV> struct World {
             SweepV sA = sweep(bA, salpha0), sB = sweep(bB, salpha0);
             if (sA.alpha0 < sB.alpha0) { sweep_advance(sA, sB.alpha0); sweep_store(bA, sA, salpha0); }
             else if (sB.alpha0 < sA.alpha0) { sweep_advance(sB, sA.alpha0); sweep_store(bB, sB, salpha0); }
-            sh.tcand[tn] = c; sh.tsA[tn] = sA; sh.tsB[tn] = sB;
+            sh.tcand[tn] = c; sh.u.toi.tsA[tn] = sA; sh.u.toi.tsB[tn] = sB;
             sh.plan[np] = tn; sh.pslot[np++] = c;
             ++tn;
         }
         sh.tn = tn; sh.np = np;
     }
     // returns true when an event was processed that needs FindNewContacts
-    __device__ void toi_event(float dt) {
+    __device__ __forceinline__ void toi_event(float dt) {
         float* salpha0 = sh.salpha0;
         int minC = NULLN; float minAlpha = 1.0f;
         for (int k = 0; k < sh.np; ++k) {
@@ -1245,8 +1286,8 @@ template <int ENV> struct World {
             if (sh.plan[k] == -2) alpha = S.ctoi[c];
             else {
                 int i = sh.plan[k];
-                float alpha0 = sh.tsA[i].alpha0;   // both sweeps share alpha0 after the sync
-                TOIOut o = sh.tout[i];
+                float alpha0 = sh.u.toi.tsA[i].alpha0;   // both sweeps share alpha0 after the sync
+                TOIOut o = sh.u.toi.tout[i];
                 if (o.state == 3) alpha = fmin_(alpha0 + (1.0f - alpha0) * o.t, 1.0f);
                 else alpha = 1.0f;
                 S.ctoi[c] = alpha;
@@ -1306,7 +1347,7 @@ template <int ENV> struct World {
                 island_add_body(is, other);
             }
         }
-        island_solve_toi(is, (1.0f - minAlpha) * dt, is.index[bA], is.index[bB], sh.vcs, sh.pcs, salpha0);
+        island_solve_toi(is, (1.0f - minAlpha) * dt, is.index[bA], is.index[bB], sh.u.sol.vcs, sh.u.sol.pcs, salpha0);
         for (int i = 0; i < is.nb; ++i) {
             int body = is.bodies[i];
             if (!is_dyn(body)) continue;
@@ -1318,7 +1359,7 @@ template <int ENV> struct World {
         }
         sh.toi_fnc = 1;
     }
-    __device__ void solve_toi_coop(float dt) {
+    __device__ __forceinline__ void solve_toi_coop(float dt) {
         if (tid == 0) {
             for (int i = 0; i < 4; ++i) sh.salpha0[i] = 0.0f;
             for (int b = 0; b < ND; ++b) S.alpha0[b] = 0.0f;
@@ -1334,7 +1375,7 @@ template <int ENV> struct World {
                 int fa = S.cfa[c], fb = S.cfb[c];
                 DProxy pA = {T.shape[fa].v, T.shape[fa].count, T.shape[fa].radius};
                 DProxy pB = {T.shape[fb].v, T.shape[fb].count, T.shape[fb].radius};
-                sh.tout[i] = time_of_impact(pA, pB, sh.tsA[i], sh.tsB[i]);
+                sh.u.toi.tout[i] = time_of_impact(pA, pB, sh.u.toi.tsA[i], sh.u.toi.tsB[i]);
             }
             __syncthreads();
             if (tid == 0) toi_event(dt);
@@ -1345,20 +1386,25 @@ template <int ENV> struct World {
     }
 
     // b2World::Step(1/50, 180, 60), cooperative (every thread of the wave calls it)
-    __device__ void world_step_coop() {
+    __device__ __forceinline__ void world_step_coop() {
         const float dt = 1.0f / 50;
         if (S.newFixture) {
             __syncthreads();
             if (tid == 0) S.newFixture = 0;
             find_new_contacts_coop();   // begins with a barrier-separated read of moveBuf
         }
+        MRP_STAMP(2);
         float inv_dt = 1.0f / dt;
         float dtRatio = S.inv_dt0 * dt;
         collide_coop();
+        MRP_STAMP(3);
         if (tid == 0) solve_serial(dt, dtRatio);
         __syncthreads();
+        MRP_STAMP(4);
         find_new_contacts_coop();
+        MRP_STAMP(5);
         solve_toi_coop(dt);
+        MRP_STAMP(6);
         if (tid == 0) {
             S.inv_dt0 = inv_dt;
             for (int b = 0; b < ND; ++b) { S.fx[b] = 0.0f; S.fy[b] = 0.0f; S.tq[b] = 0.0f; }

@@ -118,6 +118,9 @@ int mrp_set_state(mrp_ctx* ctx, const uint32_t* in);
 /* Device self-test of the glibc-faithful sinf/cosf used by every b2Rot::Set on the GPU:
  * evaluates them on device `device` for n host inputs (host output arrays). */
 int mrp_selftest_sincos(int device, const float* x, float* sin_out, float* cos_out, int n);
+/* Diagnostic builds (-DMRP_STAMPS) only: per-phase cycle totals of thread 0 since the last call
+ * (returns MRP_E_STATE in the shipped build). */
+int mrp_debug_stamps(int device, uint64_t* out16);
 
 #ifdef __cplusplus
 }
