@@ -34,28 +34,21 @@ ALGO_BYTES = {0: 1657, 1: 3547, 2: 3613, 3: 3613, 4: 6085}
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 
 
-def cpu_baseline(env_id: int, lanes: int = 256, steps: int = 1500) -> dict:
-    """Time the CPU oracle (plain-C restatement, one core) on a bounded sample."""
-    from gym_puzzles_amd.spawn import reference_draws
-    from oracle.oracle import OracleEnv, rng_u01  # noqa: F401  (test infrastructure: baseline leg only)
-    rs = np.random.RandomState(17)
-    envs = [OracleEnv(env_id) for _ in range(lanes)]
-    act_dim = envs[0].act_dim
-    for l, e in enumerate(envs):
-        e.reset(reference_draws(env_id, np.random.RandomState(17 + l)), rs.uniform(-1, 1, act_dim).astype(np.float32))
-    acts = rs.uniform(-1, 1, size=(steps, lanes, act_dim)).astype(np.float32)
-    t0 = time.perf_counter()
-    n = 0
-    for t in range(steps):
-        for l, e in enumerate(envs):
-            _, _, done, _ = e.step(acts[t, l])
-            n += 1
-            if done:
-                e.reset(reference_draws(env_id, np.random.RandomState(10_000 + n)), acts[t, l])
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{ENV_NAMES[env_id]}: {lanes} lanes x {steps} steps of the C oracle (oracle/), 1 host core, "
-                      f"random actions, {dt:.1f} s"}
+def cpu_baseline(env_id: int, lanes: int, seed: int, target_s: float = 20.0) -> dict:
+    """Time the CPU oracle (plain-C restatement, OpenMP over lanes) on a bounded sample of the
+    same workload: same env, same lane count, same counter-RNG actions/spawns and auto-reset as
+    the GPU run, for as many steps as fit in about `target_s` seconds of wall time."""
+    from gym_puzzles_amd.spawn import draw_bounds
+    from oracle.oracle import batch_run  # test infrastructure: baseline leg only
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)))
+    bounds = draw_bounds(env_id)
+    n, dt = batch_run(env_id, min(lanes, 32 * threads), 20, seed, bounds, threads=threads)    # calibrate
+    rate = n / max(dt, 1e-6)
+    steps = int(max(20, min(3000, target_s * rate / lanes)))
+    n, dt = batch_run(env_id, lanes, steps, seed, bounds, threads=threads)
+    return {"value": n / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{ENV_NAMES[env_id]}: {lanes} lanes x {steps} steps (device-RNG actions and spawns, "
+                      f"auto-reset) of the C oracle (oracle/), {threads} OpenMP threads, {dt:.1f} s"}
 
 
 def load_traffic(env_id: int, lanes: int):
@@ -88,6 +81,7 @@ def main():
     import torch.distributed as dist
 
     from gym_puzzles_amd import Batch
+    from gym_puzzles_amd.dist import Shard, StepGather
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -117,18 +111,14 @@ def main():
     done = torch.zeros(L, dtype=torch.uint8, device=dev)
     trunc = torch.zeros(L, dtype=torch.uint8, device=dev)
     # one contiguous buffer per rank for the gather: [obs | reward | done] as float32
-    packed = torch.zeros((L, O + 2), dtype=torch.float32, device=dev)
-    gathered = [torch.zeros_like(packed) for _ in range(world)] if (distributed and rank == 0) else None
+    gather = StepGather(Shard(rank, world, L), O, dev) if distributed and not args.no_gather else None
 
     b.reset()   # device-RNG spawns for every lane (seeded by global lane id)
 
     def one_step():
         b.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), trunc.data_ptr())
-        if distributed and not args.no_gather:
-            packed[:, :O].copy_(obs)
-            packed[:, O].copy_(rew)
-            packed[:, O + 1].copy_(done)
-            dist.gather(packed, gathered, dst=0)
+        if gather is not None:
+            gather(obs, rew, done)
 
     for _ in range(args.warmup):
         one_step()
@@ -144,11 +134,8 @@ def main():
         ev[k][0].record(stream)
         b.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), trunc.data_ptr())
         ev[k][1].record(stream)
-        if distributed and not args.no_gather:
-            packed[:, :O].copy_(obs)
-            packed[:, O].copy_(rew)
-            packed[:, O + 1].copy_(done)
-            dist.gather(packed, gathered, dst=0)
+        if gather is not None:
+            gather(obs, rew, done)
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()
@@ -191,7 +178,7 @@ def main():
             "diagnostics": {"toi_events_total": toi, "position_iterations_total": pos},
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.env)
+            line["cpu_baseline"] = cpu_baseline(args.env, L, args.seed)
         print(json.dumps(line), flush=True)
     b.close()
     if distributed:

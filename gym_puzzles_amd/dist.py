@@ -1,0 +1,75 @@
+"""Multi-GPU layout of the batched step: one process per GPU, lanes sharded contiguously.
+
+Worlds are independent, so the physics never exchanges data between GPUs.
+Rank r owns global lanes [r*L, (r+1)*L) and passes ``lane_offset = r*L`` to ``mrp_create``;
+the device RNG is keyed by the global lane id, so every lane's trajectory is identical at any
+GPU count.  The only collective is the per-step hand-over of (obs, reward, done) to the
+policy rank: each rank packs them into ONE contiguous float32 buffer [L, obs_dim + 2] (done as
+0.0/1.0) and ``torch.distributed.gather``s it to rank 0 (RCCL turns this into root receives +
+peer sends, one message per peer over its own xGMI link).  With a policy replica on every
+rank use ``all_gather`` instead (``StepGather(..., to_all=True)``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+
+@dataclass(frozen=True)
+class Shard:
+    rank: int
+    world: int
+    lanes_per_rank: int
+
+    @property
+    def lane_offset(self) -> int:
+        return self.rank * self.lanes_per_rank
+
+    @property
+    def global_lanes(self) -> int:
+        return self.world * self.lanes_per_rank
+
+    def lanes(self) -> range:
+        return range(self.lane_offset, self.lane_offset + self.lanes_per_rank)
+
+
+def shard_from_env(lanes_per_rank: int) -> Shard:
+    import os
+    return Shard(int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")), lanes_per_rank)
+
+
+class StepGather:
+    """Packs one step's outputs of this rank and gathers every rank's block to rank 0."""
+
+    def __init__(self, shard: Shard, obs_dim: int, device, group=None, to_all: bool = False):
+        import torch
+        self.shard, self.obs_dim, self.group, self.to_all = shard, obs_dim, group, to_all
+        L = shard.lanes_per_rank
+        self.packed = torch.zeros((L, obs_dim + 2), dtype=torch.float32, device=device)
+        root = shard.rank == 0 or to_all
+        self.blocks = [torch.zeros_like(self.packed) for _ in range(shard.world)] if root else None
+
+    def pack(self, obs, reward, done):
+        O = self.obs_dim
+        self.packed[:, :O].copy_(obs)
+        self.packed[:, O].copy_(reward)
+        self.packed[:, O + 1].copy_(done)
+        return self.packed
+
+    def __call__(self, obs, reward, done):
+        """Returns (obs [G, O], reward [G], done [G]) over all G global lanes on rank 0 (every
+        rank with to_all), None elsewhere.  Single-process: no collective."""
+        import torch
+        import torch.distributed as dist
+        p = self.pack(obs, reward, done)
+        if self.shard.world == 1:
+            full = p
+        else:
+            if self.to_all:
+                dist.all_gather(self.blocks, p, group=self.group)
+            else:
+                dist.gather(p, self.blocks if self.shard.rank == 0 else None, dst=0, group=self.group)
+            if self.blocks is None:
+                return None
+            full = torch.cat(self.blocks, dim=0)
+        O = self.obs_dim
+        return full[:, :O], full[:, O], full[:, O + 1] != 0

@@ -551,3 +551,89 @@ int or_proxy_ids(const OrEnv* e, int* out) {
     for (int i = 0; i < 4; ++i) k = push_proxies(e->walls[i], out, k);
     return k;
 }
+
+/* Mass data of dynamic body i (blocks, then agents): mass, rotational inertia about the
+ * body origin (b2Body::GetInertia), local centre x, y.  Known-answer tests. */
+int or_body_mass(const OrEnv* e, int i, float* out4) {
+    int nb = e->cfg.n_blocks, na = e->cfg.n_agents;
+    if (!e->have_bodies || i < 0 || i >= nb + na) return -1;
+    const Body* b = i < nb ? e->blocks[i] : e->agents[i - nb];
+    out4[0] = b->mass; out4[1] = b2o_inertia(b);
+    out4[2] = b->sweep.localCenter.x; out4[3] = b->sweep.localCenter.y;
+    return 0;
+}
+
+/* Batched run with the device path's synthetic-input scheme (mrp_kernels.hip k_step/k_reset,
+ * actions == NULL, draws == NULL, auto-reset on): lane l is global lane lane_offset + l;
+ * reset e of a lane draws spawn d from RNG stream 1 and its action component j from stream 2
+ * (counter e*64 + d / j); step s of a lane (counted over the lane's lifetime) takes action
+ * component j from stream 3 (counter s*64 + j); done or TimeLimit -> reset.  Lanes are split
+ * over `threads` OpenMP threads.  Used as bench.py's CPU baseline and as the full-size parity
+ * checker of the device auto-reset path.  Returns env-steps done; *seconds = wall time of the
+ * stepping loop (initial resets and env creation excluded).  Optional outputs (NULL to skip):
+ * max_steps <= 0 uses the registered TimeLimit.  bodies [n_lanes][6*(n_blocks+n_agents)] final state, rsum [n_lanes] summed float32(reward),
+ * resets [n_lanes] episodes started. */
+#include <omp.h>
+long or_batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_t lane_offset, const double* lo,
+                  const double* hi, int max_steps, int threads, double* seconds, float* bodies, double* rsum,
+                  int* resets) {
+    if (!valid(env_id) || n_lanes <= 0 || steps < 0) return -1;
+    const Cfg cfg = CFGS[env_id];
+    const int limit = max_steps > 0 ? max_steps : cfg.max_steps;
+    const int nbody = 6 * (cfg.n_blocks + cfg.n_agents);
+    OrEnv** envs = (OrEnv**)calloc((size_t)n_lanes, sizeof(OrEnv*));
+    int* episode = (int*)calloc((size_t)n_lanes, sizeof(int));
+    if (threads > 0) omp_set_num_threads(threads);
+    double t0 = 0.0, t1 = 0.0;
+    long total = 0;
+#pragma omp parallel
+    {
+        double draws[16], obs[128], rew; float act[16]; int done, kind;
+#pragma omp for schedule(static)
+        for (int l = 0; l < n_lanes; ++l) {
+            const uint64_t g = lane_offset + (uint64_t)l;
+            envs[l] = or_create(env_id);
+            for (int d = 0; d < cfg.n_draws; ++d) draws[d] = lo[d] + (hi[d] - lo[d]) * or_rng_u01(seed, g, 1, (uint64_t)d);
+            for (int j = 0; j < cfg.act_dim; ++j) act[j] = (float)(-1.0 + 2.0 * or_rng_u01(seed, g, 2, (uint64_t)j));
+            or_reset(envs[l], draws, act, obs);
+            episode[l] = 1;
+        }
+#pragma omp single
+        t0 = omp_get_wtime();
+#pragma omp for schedule(static) reduction(+:total)
+        for (int l = 0; l < n_lanes; ++l) {
+            OrEnv* e = envs[l];
+            const uint64_t g = lane_offset + (uint64_t)l;
+            int elapsed = 0;
+            double rs = 0.0;
+            for (int s = 0; s < steps; ++s) {
+                for (int j = 0; j < cfg.act_dim; ++j)
+                    act[j] = (float)(-1.0 + 2.0 * or_rng_u01(seed, g, 3, (uint64_t)s * 64 + (uint64_t)j));
+                or_step(e, act, obs, &rew, &done, &kind);
+                rs += (double)(float)rew;
+                ++total;
+                if (done || ++elapsed >= limit) {
+                    const uint64_t ctr = (uint64_t)episode[l] * 64;
+                    for (int d = 0; d < cfg.n_draws; ++d)
+                        draws[d] = lo[d] + (hi[d] - lo[d]) * or_rng_u01(seed, g, 1, ctr + (uint64_t)d);
+                    for (int j = 0; j < cfg.act_dim; ++j) act[j] = (float)(-1.0 + 2.0 * or_rng_u01(seed, g, 2, ctr + (uint64_t)j));
+                    or_reset(e, draws, act, obs);
+                    ++episode[l];
+                    elapsed = 0;
+                }
+            }
+            if (rsum) rsum[l] = rs;
+        }
+#pragma omp single
+        t1 = omp_get_wtime();
+#pragma omp for schedule(static)
+        for (int l = 0; l < n_lanes; ++l) {
+            if (bodies) or_get_bodies(envs[l], bodies + (size_t)l * nbody);
+            if (resets) resets[l] = episode[l];
+            or_destroy(envs[l]);
+        }
+    }
+    *seconds = t1 - t0;
+    free(envs); free(episode);
+    return total;
+}

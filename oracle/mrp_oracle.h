@@ -43,6 +43,10 @@ int or_contact_count(const OrEnv* e);
 void or_counters(const OrEnv* e, long* toi_events, long* pos_iters);
 /* proxy ids of all fixtures in creation order (blocks, agents, walls) */
 int or_proxy_ids(const OrEnv* e, int* out);
+int or_body_mass(const OrEnv* e, int i, float* out4);
+long or_batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_t lane_offset, const double* lo,
+                  const double* hi, int max_steps, int threads, double* seconds, float* bodies, double* rsum,
+                  int* resets);
 
 /* glibc-faithful math exported for tests */
 float or_sinf(float x);

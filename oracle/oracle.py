@@ -66,6 +66,10 @@ def lib():
         L.or_cosf.restype = c_float
         L.or_rng_u01.argtypes = [ctypes.c_uint64] * 4
         L.or_rng_u01.restype = c_double
+        L.or_body_mass.argtypes = [P, c_int, P]
+        L.or_body_mass.restype = c_int
+        L.or_batch_run.argtypes = [c_int, c_int, c_int, ctypes.c_uint64, ctypes.c_uint64, P, P, c_int, c_int, P, P, P, P]
+        L.or_batch_run.restype = ctypes.c_long
         _lib = L
     return _lib
 
@@ -134,6 +138,13 @@ class OracleEnv:
         lib().or_counters(self._h, _ptr(a), _ptr(b))
         return int(a[0]), int(b[0])
 
+    def body_mass(self, i: int):
+        """(mass, inertia about the body origin, local centre x, y) of dynamic body i."""
+        out = np.zeros(4, np.float32)
+        if lib().or_body_mass(self._h, i, _ptr(out)) != 0:
+            raise IndexError(i)
+        return tuple(float(v) for v in out)
+
     def proxy_ids(self) -> np.ndarray:
         out = np.zeros(64, np.int32)
         n = lib().or_proxy_ids(self._h, _ptr(out))
@@ -142,3 +153,27 @@ class OracleEnv:
 
 def rng_u01(seed: int, lane: int, stream: int, counter: int) -> float:
     return lib().or_rng_u01(seed, lane, stream, counter)
+
+
+def batch_run(env_id: int, lanes: int, steps: int, seed: int, bounds, threads: int = 1, lane_offset: int = 0,
+              outputs: bool = False, max_steps: int = 0):
+    """Run `lanes` oracle envs for `steps` steps each with the device path's synthetic inputs
+    (counter RNG actions and spawns, auto-reset; see or_batch_run) on `threads` OpenMP threads.
+    Returns (env_steps, seconds) or, with outputs=True, (env_steps, seconds, bodies, reward_sums,
+    episodes)."""
+    lo = np.ascontiguousarray([b[0] for b in bounds], dtype=np.float64)
+    hi = np.ascontiguousarray([b[1] for b in bounds], dtype=np.float64)
+    sec = np.zeros(1, np.float64)
+    L = lib()
+    nb = 6 * (L.or_n_agents(env_id) + L.or_n_blocks(env_id))
+    bodies = np.zeros((lanes, nb), np.float32) if outputs else None
+    rsum = np.zeros(lanes, np.float64) if outputs else None
+    eps = np.zeros(lanes, np.int32) if outputs else None
+    P = lambda a: None if a is None else _ptr(a)  # noqa: E731
+    n = L.or_batch_run(env_id, lanes, steps, seed, lane_offset, _ptr(lo), _ptr(hi), max_steps, threads, _ptr(sec),
+                       P(bodies), P(rsum), P(eps))
+    if n < 0:
+        raise ValueError("or_batch_run: bad arguments")
+    if outputs:
+        return int(n), float(sec[0]), bodies, rsum, eps
+    return int(n), float(sec[0])

@@ -1,0 +1,249 @@
+"""GPU parity tests: the HIP step (libmrp.so, through the C ABI) against the CPU oracle.
+
+The bar is bit-exactness: the engine runs float32 with the same operation order as the
+oracle (both built without FMA contraction), so obs, reward, done and every body's state must
+be identical, not merely close.  Sizes: small lane counts over hundreds of steps for the
+step-by-step comparisons, and BASELINE.json's 4096 lanes for the device auto-reset path
+(final state + reward sums vs the oracle's multi-threaded batch runner).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+from gym_puzzles_amd.spawn import draw_bounds, reference_draws
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+ENVS = range(5)
+
+
+@pytest.fixture(scope="module")
+def orc(oracle_lib):
+    from oracle import oracle
+    return oracle
+
+
+def _eq(name, g, c):
+    g, c = np.asarray(g), np.asarray(c)
+    bad = ~((g == c) | (np.isnan(g) & np.isnan(c)))
+    if bad.any():
+        i = tuple(np.argwhere(bad)[0])
+        raise AssertionError(f"{name}: {int(bad.sum())} elements differ, first at {i}: gpu {g[i]!r} oracle {c[i]!r}")
+
+
+@pytest.mark.parametrize("env_id", ENVS)
+def test_step_parity_host_inputs(gpu_lib, orc, env_id):
+    """64 lanes x 200 steps with host spawns/actions; finished lanes reset through the mask."""
+    from gym_puzzles_amd import Batch
+    lanes, steps = 64, 200
+    rs_d = [np.random.RandomState(17 + l) for l in range(lanes)]
+    rs_a = np.random.RandomState(1017)
+    b = Batch(env_id, lanes)
+    envs = [orc.OracleEnv(env_id) for _ in range(lanes)]
+    draws = np.stack([reference_draws(env_id, r) for r in rs_d])
+    acts = rs_a.uniform(-1, 1, size=(lanes, b.act_dim)).astype(np.float32)
+    _eq("reset obs", b.reset(draws, acts), np.stack([o.reset(draws[l], acts[l]) for l, o in enumerate(envs)]))
+    for t in range(steps):
+        a = rs_a.uniform(-1, 1, size=(lanes, b.act_dim)).astype(np.float32)
+        obs, rew, done, trunc = b.step(a)
+        res = [o.step(a[l]) for l, o in enumerate(envs)]
+        _eq(f"obs@{t}", obs, np.stack([r[0] for r in res]).astype(np.float32))
+        _eq(f"reward@{t}", rew, np.array([r[1] for r in res]).astype(np.float32))
+        _eq(f"done@{t}", done, np.array([r[2] for r in res], np.uint8))
+        _eq(f"status@{t}", b.status, np.array([r[3] for r in res], np.uint8))
+        _eq(f"bodies@{t}", b.bodies(), np.stack([o.bodies() for o in envs]))
+        fl = b.flags()
+        _eq(f"flags@{t}", fl, np.stack([np.r_[o.flags()[0], o.flags()[1]] for o in envs]).astype(np.int32))
+        fin = done.astype(bool) | trunc.astype(bool)
+        if fin.any():
+            d2 = np.stack([reference_draws(env_id, r) for r in rs_d])
+            a2 = rs_a.uniform(-1, 1, size=(lanes, b.act_dim)).astype(np.float32)
+            o2 = b.reset(d2, a2, mask=fin).copy()
+            for l in np.nonzero(fin)[0]:
+                _eq(f"reset obs@{t} lane {l}", o2[l], envs[l].reset(d2[l], a2[l]).astype(np.float32))
+    toi = sum(o.counters()[0] for o in envs)
+    pos = sum(o.counters()[1] for o in envs)
+    assert b.counters() == (toi, pos)
+    b.close()
+
+
+@pytest.mark.parametrize("env_id", ENVS)
+def test_golden_trajectory(gpu_lib, env_id):
+    """The committed fixtures (tests/golden/traj_env*.npz) reproduce on the GPU."""
+    from gym_puzzles_amd import Batch
+    z = np.load(os.path.join(GOLDEN, f"traj_env{env_id}.npz"))
+    lanes = z["draws0"].shape[0]
+    b = Batch(env_id, lanes)
+    _eq("obs0", b.reset(z["draws0"], z["act0"]), z["obs0"])
+    for t in range(z["acts"].shape[0]):
+        obs, rew, done, _ = b.step(z["acts"][t])
+        _eq(f"obs@{t}", obs, z["obs"][t])
+        _eq(f"reward@{t}", rew, z["reward"][t])
+        _eq(f"done@{t}", done, z["done"][t])
+        _eq(f"bodies@{t}", b.bodies(), z["bodies"][t])
+        if done.any():
+            m = done.astype(bool)
+            o2 = b.reset(z["rdraws"][t], z["racts"][t], mask=m).copy()
+            _eq(f"reset obs@{t}", o2[m], z["robs"][t][m])
+    b.close()
+
+
+def test_reference_test_flow_v0_seed17(gpu_lib):
+    """gym_puzzles/tests/test_env.py flow (seed 17) on v0; expected values from the fixture."""
+    from gym_puzzles_amd import Batch
+    from gym_puzzles_amd.seeding import Box
+    z = np.load(os.path.join(GOLDEN, "scenario_v0_seed17.npz"))
+    b = Batch(0, 1)
+    sp = Box(-1.0, 1.0, shape=(6,))
+    np.random.seed(0)
+    b.reset(reference_draws(0)[None], sp.sample()[None])
+    _eq("obs0", b.reset(z["draws"][None], z["act0"][None]), z["obs0"][None])
+    for t in range(z["acts"].shape[0]):
+        obs, rew, _, _ = b.step(z["acts"][t][None])
+        _eq(f"obs@{t}", obs[0], z["obs"][t])
+        _eq(f"reward@{t}", rew[0], np.float32(z["reward"][t]))
+    _eq("bodies", b.bodies()[0], z["bodies"])
+    b.close()
+
+
+@pytest.mark.parametrize("env_id", ENVS)
+def test_device_autoreset_full_size(gpu_lib, orc, env_id):
+    """BASELINE.json-size batch (4096 lanes) on the device-input path: counter-RNG spawns and
+    actions, TimeLimit 64 so every lane auto-resets several times; final body state and per-lane
+    reward sums must equal the oracle's batch runner bit for bit."""
+    from gym_puzzles_amd import Batch
+    lanes, steps, limit = 4096, 200, 64
+    b = Batch(env_id, lanes, seed=17)
+    b.set_auto_reset(True)
+    b.set_time_limit(limit)
+    b.reset()
+    rsum = np.zeros(lanes, np.float64)
+    n_fin = 0
+    for _ in range(steps):
+        _, rew, done, _ = b.step()
+        rsum += rew.astype(np.float64)
+        n_fin += int(done.sum())
+    threads = min(16, os.cpu_count() or 1)
+    n, _, bodies, orsum, eps = orc.batch_run(env_id, lanes, steps, 17, draw_bounds(env_id), threads=threads,
+                                             outputs=True, max_steps=limit)
+    assert n == lanes * steps
+    assert n_fin == int((eps - 1).sum()) and n_fin >= 3 * lanes
+    _eq("bodies", b.bodies(), bodies)
+    _eq("reward sums", rsum, orsum)
+    b.close()
+
+
+def test_lane_offset_invariance(gpu_lib):
+    """A shard with lane_offset = k steps exactly like lanes k.. of the unsharded batch."""
+    from gym_puzzles_amd import Batch
+    full = Batch(2, 256, seed=5)
+    half = Batch(2, 128, seed=5, lane_offset=128)
+    for b in (full, half):
+        b.set_auto_reset(True)
+        b.set_time_limit(40)
+        b.reset()
+    for _ in range(100):
+        of, rf, df, _ = full.step()
+        oh, rh, dh, _ = half.step()
+        _eq("obs", oh, of[128:])
+        _eq("reward", rh, rf[128:])
+        _eq("done", dh, df[128:])
+    _eq("bodies", half.bodies(), full.bodies()[128:])
+
+
+def test_autoreset_terminal_obs_matches_manual_reset(gpu_lib):
+    """Auto-reset (SB3 semantics) == stepping without it and resetting the finished lanes by mask."""
+    from gym_puzzles_amd import Batch
+    lanes = 96
+    a = Batch(0, lanes, seed=9)
+    m = Batch(0, lanes, seed=9)
+    for b in (a, m):
+        b.set_time_limit(30)
+        b.reset()
+    a.set_auto_reset(True)
+    rs = np.random.RandomState(4)
+    for _ in range(75):
+        act = rs.uniform(-1, 1, size=(lanes, 6)).astype(np.float32)
+        oa, ra, da, ta = a.step(act, want_terminal_obs=True)
+        om, rm, dm, tm = m.step(act)
+        _eq("reward", ra, rm)
+        _eq("done", da, dm)
+        _eq("truncated", ta, tm)
+        fin = dm.astype(bool)
+        if fin.any():
+            _eq("terminal obs", a.terminal_obs[fin], om[fin])
+            om = m.reset(mask=fin).copy()                    # device-RNG reset of those lanes
+        _eq("obs", oa, om)
+
+
+def test_state_round_trip(gpu_lib):
+    from gym_puzzles_amd import Batch
+    b = Batch(4, 32, seed=3)
+    b.set_auto_reset(True)
+    b.reset()
+    for _ in range(40):
+        b.step()
+    snap = b.get_state().copy()
+    runs = []
+    for _ in range(2):
+        b.set_state(snap)
+        for _ in range(30):
+            obs, rew, _, _ = b.step()
+        runs.append((obs.copy(), rew.copy(), b.bodies()))
+    for x, y in zip(*runs):
+        _eq("replay", x, y)
+
+
+def test_step_before_reset_fails_loudly(gpu_lib):
+    from gym_puzzles_amd import Batch, MrpError
+    b = Batch(0, 4)
+    with pytest.raises(MrpError, match="before reset"):
+        b.step()
+
+
+def test_device_sincos_matches_glibc(gpu_lib, orc):
+    """The device sinf/cosf restatement equals the host glibc sinf/cosf (the oracle's)."""
+    from gym_puzzles_amd._native import selftest_sincos
+    rs = np.random.RandomState(0)
+    x = np.concatenate([
+        rs.uniform(-10, 10, 200000), rs.uniform(-1e4, 1e4, 50000), rs.uniform(-1e30, 1e30, 2000),
+        np.arange(-64, 65) * (np.pi / 4), np.array([0.0, -0.0, 1e-30, -1e-30, 1e-45, np.pi, 3e38, -3e38]),
+    ]).astype(np.float32)
+    s, c = selftest_sincos(x)
+    L = orc.lib()
+    step = 37
+    idx = np.r_[np.arange(0, x.size, step), np.arange(x.size - 200, x.size)]
+    es = np.array([L.or_sinf(float(x[i])) for i in idx], np.float32)
+    ec = np.array([L.or_cosf(float(x[i])) for i in idx], np.float32)
+    _eq("sinf", s[idx], es)
+    _eq("cosf", c[idx], ec)
+
+
+def test_step_device_with_torch_stream(gpu_lib):
+    """mrp_step_device on torch tensors, on a torch stream, equals the host-pointer path."""
+    import torch
+
+    from gym_puzzles_amd import Batch
+    lanes = 128
+    h = Batch(2, lanes, seed=11)
+    d = Batch(2, lanes, seed=11)
+    for b in (h, d):
+        b.set_auto_reset(True)
+        b.reset()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(dev)
+    d.set_stream(s.cuda_stream)
+    obs = torch.zeros((lanes, d.obs_dim), device=dev)
+    rew = torch.zeros(lanes, device=dev)
+    done = torch.zeros(lanes, dtype=torch.uint8, device=dev)
+    for _ in range(50):
+        h.step()
+        with torch.cuda.stream(s):
+            d.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr())
+    s.synchronize()
+    _eq("obs", obs.cpu().numpy(), h.obs)
+    _eq("reward", rew.cpu().numpy(), h.reward)
+    _eq("done", done.cpu().numpy(), h.done)
