@@ -44,7 +44,7 @@ def cpu_baseline(env_id: int, lanes: int, seed: int, target_s: float = 20.0) -> 
     bounds = draw_bounds(env_id)
     n, dt = batch_run(env_id, min(lanes, 32 * threads), 20, seed, bounds, threads=threads)    # calibrate
     rate = n / max(dt, 1e-6)
-    steps = int(max(20, min(3000, target_s * rate / lanes)))
+    steps = int(max(20, min(20000, target_s * rate / lanes)))
     n, dt = batch_run(env_id, lanes, steps, seed, bounds, threads=threads)
     return {"value": n / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"{ENV_NAMES[env_id]}: {lanes} lanes x {steps} steps (device-RNG actions and spawns, "
