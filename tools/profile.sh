@@ -14,5 +14,5 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- python3 bench.py $ARGS > $OUT/write.log 2>&1
 python3 tools/traffic.py $OUT/fetch $OUT/write $ENV 4096 profiles/pmc_traffic.json
 cp "$(find $OUT/kt -name '*kernel_stats.csv' -print -quit)" profiles/${TAG}_kernel_stats.csv
-tail -1 $OUT/kt.log > profiles/${TAG}_bench_under_rocprof.json
+grep -h "\"metric\"" $OUT/kt.log > profiles/${TAG}_bench_under_rocprof.json
 echo done
