@@ -1,0 +1,137 @@
+"""Host-side env classes (gym_puzzles_amd/envs.py, vec_env.py, seeding.py).
+
+CPU: gym 0.21 seeding/Box and TimeLimit logic.  GPU: the single-env classes replay the
+reference's own test flow (gym_puzzles/tests/test_env.py) against the committed fixture, and
+the SB3-style VecEnv honours SB3's auto-reset contract.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+# ----------------------------------------------------------------------------- CPU
+def test_gym_seeding_restatement_properties():
+    from gym_puzzles_amd.seeding import Box, _bigint_from_bytes, _int_list_from_bigint, create_seed, np_random
+    # _bigint_from_bytes always pads with a zero word (gym 0.21 quirk)
+    assert _bigint_from_bytes(b"\x01\x00\x00\x00") == 1
+    assert _int_list_from_bigint(2 ** 32 + 5) == [5, 1] and _int_list_from_bigint(0) == [0]
+    assert create_seed(17) == 17 and create_seed(2 ** 64 + 3) == 3
+    r1, s1 = np_random(17)
+    r2, _ = np_random(17)
+    assert s1 == 17 and r1.uniform() == r2.uniform()
+    with pytest.raises(ValueError):
+        np_random(-1)
+    sp = Box(-1.0, 1.0, shape=(6,))
+    sp.seed(17)
+    a = sp.sample()
+    assert a.dtype == np.float32 and a.shape == (6,) and np.all(np.abs(a) <= 1) and sp.contains(a)
+    sp.seed(17)
+    assert np.array_equal(sp.sample(), a)
+
+
+def test_time_limit_wrapper():
+    from gym_puzzles_amd.envs import TimeLimit
+
+    class Fake:
+        def reset(self):
+            return 0
+
+        def step(self, a):
+            return 0, 1.0, a == "end", {}
+
+    env = TimeLimit(Fake(), 3)
+    env.reset()
+    assert env.step("x")[2] is False and env.step("x")[2] is False
+    _, _, done, info = env.step("x")
+    assert done and info["TimeLimit.truncated"] is True
+    env.reset()
+    env.step("x")
+    env.step("x")
+    _, _, done, info = env.step("end")
+    assert done and info["TimeLimit.truncated"] is False
+
+
+def test_product_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a HIP device is visible")
+    from gym_puzzles_amd import MrpError, make
+    with pytest.raises(MrpError):
+        make("MultiRobotPuzzle-v0")
+
+
+# ----------------------------------------------------------------------------- GPU
+@pytest.mark.gpu
+def test_single_env_reference_test_flow(gpu_lib):
+    """test_env.py:12-29 flow on gym_puzzles_amd.make('MultiRobotPuzzle-v0'), seed 17."""
+    from gym_puzzles_amd import make
+    z = np.load(os.path.join(GOLDEN, "scenario_v0_seed17.npz"))
+    np.random.seed(0)
+    env = make("MultiRobotPuzzle-v0")        # constructor runs reset() once, like the reference
+    np.random.seed(17)
+    assert env.seed(17) == [17]
+    env.action_space.seed(17)
+    obs = env.reset()
+    assert obs.dtype == np.float64 and obs.shape == env.observation_space.shape == (28,)
+    assert np.array_equal(obs.astype(np.float32), z["obs0"])
+    for t in range(z["acts"].shape[0]):
+        a = env.action_space.sample()
+        assert np.array_equal(a, z["acts"][t])
+        obs, rew, done, info = env.step(a)
+        assert np.array_equal(obs.astype(np.float32), z["obs"][t])
+        assert np.float32(rew) == np.float32(z["reward"][t]) and done is False and info == {}
+    assert np.array_equal(env.unwrapped.bodies().ravel(), z["bodies"])
+    assert env.get_deltaAgent() == 10 and env.get_blkDist() == 0.025
+    env.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,obs_dim,act_dim", [("MultiRobotPuzzleHeavy-v0", 40, 15), ("MultiRobotPuzzle-v2", 39, 4),
+                                                  ("MultiRobotPuzzleHeavy-v2", 39, 4),
+                                                  ("MultiRobotPuzzleHeavy-v2-3block", 69, 4)])
+def test_single_env_spaces_and_step(gpu_lib, name, obs_dim, act_dim):
+    from gym_puzzles_amd import make
+    env = make(name)
+    assert env.observation_space.shape == (obs_dim,) and env.action_space.shape == (act_dim,)
+    env.update_params(0, 1.0)
+    o = env.reset()
+    assert o.shape == (obs_dim,)
+    for _ in range(20):
+        o, r, d, info = env.step(env.action_space.sample())
+        assert np.isfinite(o).all() and np.isfinite(r)
+    env.close()
+
+
+@pytest.mark.gpu
+def test_vec_env_sb3_contract(gpu_lib):
+    from gym_puzzles_amd import Batch, MultiRobotPuzzleVecEnv
+    n = 64
+    venv = MultiRobotPuzzleVecEnv("MultiRobotPuzzle-v0", n, seed=3, max_episode_steps=25)
+    ref = Batch(0, n, seed=3)                  # same RNG keys, no auto-reset
+    ref.set_time_limit(25)
+    o = venv.reset()
+    assert o.shape == (n, 28) and o.dtype == np.float32
+    assert np.array_equal(o, ref.reset())
+    rs = np.random.RandomState(0)
+    seen = 0
+    for _ in range(60):
+        a = rs.uniform(-1, 1, size=(n, 6)).astype(np.float32)
+        obs, rew, done, infos = venv.step(a)
+        robs, rrew, rdone, rtrunc = ref.step(a)
+        assert np.array_equal(rew, rrew) and np.array_equal(done, rdone.astype(bool))
+        for i in np.nonzero(done)[0]:
+            seen += 1
+            assert np.array_equal(infos[i]["terminal_observation"], robs[i])
+            assert infos[i]["TimeLimit.truncated"] == bool(rtrunc[i])
+        if done.any():
+            robs = ref.reset(mask=done).copy()
+        assert np.array_equal(obs, robs)
+        assert all("terminal_observation" not in infos[i] for i in np.nonzero(~done)[0])
+    assert seen >= n * 2
+    assert venv.env_method("update_params", 10, 1.01) == [None] * n
+    venv.close()

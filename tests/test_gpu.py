@@ -45,7 +45,7 @@ def test_step_parity_host_inputs(gpu_lib, orc, env_id):
     envs = [orc.OracleEnv(env_id) for _ in range(lanes)]
     draws = np.stack([reference_draws(env_id, r) for r in rs_d])
     acts = rs_a.uniform(-1, 1, size=(lanes, b.act_dim)).astype(np.float32)
-    _eq("reset obs", b.reset(draws, acts), np.stack([o.reset(draws[l], acts[l]) for l, o in enumerate(envs)]))
+    _eq("reset obs", b.reset(draws, acts), np.stack([o.reset(draws[l], acts[l]) for l, o in enumerate(envs)]).astype(np.float32))
     for t in range(steps):
         a = rs_a.uniform(-1, 1, size=(lanes, b.act_dim)).astype(np.float32)
         obs, rew, done, trunc = b.step(a)
