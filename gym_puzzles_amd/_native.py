@@ -31,7 +31,8 @@ EXPORTED = (
     "mrp_set_stream", "mrp_synchronize", "mrp_set_reward_params", "mrp_update_params", "mrp_update_goal",
     "mrp_reset", "mrp_reset_device", "mrp_step", "mrp_step_device", "mrp_set_auto_reset",
     "mrp_get_bodies", "mrp_get_flags", "mrp_counters", "mrp_state_words", "mrp_get_state", "mrp_set_state",
-    "mrp_set_time_limit", "mrp_selftest_sincos", "mrp_debug_stamps",
+    "mrp_set_time_limit", "mrp_selftest_sincos", "mrp_debug_stamps", "mrp_debug_stamps_ext",
+    "mrp_debug_trace",
 )
 
 _lib = None
@@ -79,6 +80,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.mrp_set_time_limit.argtypes = [P, i]
     L.mrp_selftest_sincos.argtypes = [i, P, P, P, i]
     L.mrp_debug_stamps.argtypes = [i, P]
+    for name, args in (("mrp_debug_stamps_ext", [i, P, P, P]), ("mrp_debug_trace", [i, P, i])):
+        if hasattr(L, name):   # diagnostics: absent from older builds
+            getattr(L, name).argtypes = args
     _lib = L
     return L
 

@@ -113,10 +113,15 @@ __global__ __launch_bounds__(BLOCK, 4) void k_step(uint32_t* state, int nl, cons
     if (lane >= nl) return;
     const uint64_t glane = lane_offset + lane;
 #ifdef MRP_STAMPS
-    if (tid == 0) sh.stamp_t = __builtin_amdgcn_s_memtime();
+    if (tid == 0) { sh.stamp_t = sh.stamp_t0 = __builtin_amdgcn_s_memtime(); sh.stamp_rt0 = __builtin_amdgcn_s_memrealtime(); }
+    if (tid < 16) sh.trace[tid] = 0;
+    long long toi0 = 0, pos0 = 0;
 #endif
     load_state<ENV>(sh.S, state, lane, tid);
     __syncthreads();
+#ifdef MRP_STAMPS
+    toi0 = sh.S.toiEvents; pos0 = sh.S.posIters;
+#endif
     MRP_STAMP(0);
     const uint64_t ctr = (uint64_t)sh.S.stepCounter * 64u;
     if (tid < D::ACT)
@@ -148,6 +153,19 @@ __global__ __launch_bounds__(BLOCK, 4) void k_step(uint32_t* state, int nl, cons
     for (int k = tid; k < D::OBS; k += BLOCK) orow[k] = sh.obs[k];
     store_state<ENV>(sh.S, state, lane, tid);
     MRP_STAMP(10);
+#ifdef MRP_STAMPS
+    if (tid == 0) {
+        unsigned long long tot = sh.stamp_t - sh.stamp_t0;
+        atomicAdd(&g_rt[0], tot);
+        atomicAdd(&g_rt[1], __builtin_amdgcn_s_memrealtime() - sh.stamp_rt0);
+        atomicMax(&g_stepmax[(sh.S.stepCounter - 1u) & 255u], tot);
+        sh.trace[11] = (uint32_t)tot;
+        sh.trace[13] = (uint32_t)(sh.S.toiEvents - toi0);
+        sh.trace[14] = (uint32_t)(sh.S.posIters - pos0);
+    }
+    __syncthreads();
+    if (tid < 16 && lane < 16384) g_trace[lane][tid] = sh.trace[tid];
+#endif
 }
 
 __global__ __launch_bounds__(256) void k_sincos(const float* x, float* s, float* c, int n) {
@@ -516,11 +534,44 @@ int mrp_debug_stamps(int device, uint64_t* out16) {
     if (!out16 || hipSetDevice(device) != hipSuccess) return MRP_E_HIP;
     if (hipDeviceSynchronize() != hipSuccess) return MRP_E_HIP;
     if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamps), 16 * sizeof(uint64_t)) != hipSuccess) return MRP_E_HIP;
-    uint64_t z[16] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) != hipSuccess) return MRP_E_HIP;
+    uint64_t z[256] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, 16 * sizeof(uint64_t)) != hipSuccess) return MRP_E_HIP;
     return MRP_OK;
 #else
     (void)device; (void)out16;
+    return MRP_E_STATE;
+#endif
+}
+
+// Diagnostic builds only: per-phase maxima, per-step slowest-lane totals (256 slots) and the
+// (s_memtime, s_memrealtime) sums of lane totals since the last call; all reset afterwards.
+int mrp_debug_stamps_ext(int device, uint64_t* pmax16, uint64_t* stepmax256, uint64_t* rt2) {
+#ifdef MRP_STAMPS
+    if (!pmax16 || !stepmax256 || !rt2 || hipSetDevice(device) != hipSuccess) return MRP_E_HIP;
+    if (hipDeviceSynchronize() != hipSuccess) return MRP_E_HIP;
+    if (hipMemcpyFromSymbol(pmax16, HIP_SYMBOL(g_pmax), 16 * sizeof(uint64_t)) != hipSuccess) return MRP_E_HIP;
+    if (hipMemcpyFromSymbol(stepmax256, HIP_SYMBOL(g_stepmax), 256 * sizeof(uint64_t)) != hipSuccess) return MRP_E_HIP;
+    if (hipMemcpyFromSymbol(rt2, HIP_SYMBOL(g_rt), 2 * sizeof(uint64_t)) != hipSuccess) return MRP_E_HIP;
+    uint64_t z[256] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_pmax), z, 16 * sizeof(uint64_t)) != hipSuccess) return MRP_E_HIP;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stepmax), z, 256 * sizeof(uint64_t)) != hipSuccess) return MRP_E_HIP;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_rt), z, 2 * sizeof(uint64_t)) != hipSuccess) return MRP_E_HIP;
+    return MRP_OK;
+#else
+    (void)device; (void)pmax16; (void)stepmax256; (void)rt2;
+    return MRP_E_STATE;
+#endif
+}
+
+// Diagnostic builds only: the last step's per-lane trace (n_lanes x 16 words, n_lanes <= 16384).
+int mrp_debug_trace(int device, uint32_t* out, int n_lanes) {
+#ifdef MRP_STAMPS
+    if (!out || n_lanes <= 0 || n_lanes > 16384 || hipSetDevice(device) != hipSuccess) return MRP_E_ARG;
+    if (hipDeviceSynchronize() != hipSuccess) return MRP_E_HIP;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace), (size_t)n_lanes * 16 * sizeof(uint32_t)) != hipSuccess) return MRP_E_HIP;
+    return MRP_OK;
+#else
+    (void)device; (void)out; (void)n_lanes;
     return MRP_E_STATE;
 #endif
 }

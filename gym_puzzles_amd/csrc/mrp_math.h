@@ -59,45 +59,45 @@ MRP_HD Xf mulT_xx(Xf A, Xf B) { Xf C; C.q = mulT_rr(A.q, B.q); C.p = mulT_rv(A.q
 // sinf/cosf in every b2Rot::Set, so sharing one exact implementation is what makes the
 // GPU trajectory bitwise equal to the CPU one.
 // ---------------------------------------------------------------------------------------
-struct SinCosT { double sign[4]; double hpi_inv, hpi, c0, c1, c2, c3, c4, s1, s2, s3; };
+// Coefficients are immediate operands (no table in memory: a data-dependent table pick
+// compiles to global loads on the device).  glibc's second table (__sincosf_table[1]) is
+// the first with c0..c4 negated and the same s1..s3, so "table 1" is the table-0 polynomial
+// with its (exactly representable) result negated; `sign[n & 3]` is {+1, -1, -1, +1}.
+constexpr double SC_HPI_INV = 0x1.45F306DC9C883p+23, SC_HPI = 0x1.921FB54442D18p0;
+constexpr double SC_C0 = 0x1p0, SC_C1 = -0x1.ffffffd0c621cp-2, SC_C2 = 0x1.55553e1068f19p-5,
+                 SC_C3 = -0x1.6c087e89a359dp-10, SC_C4 = 0x1.99343027bf8c3p-16;
+constexpr double SC_S1 = -0x1.555545995a603p-3, SC_S2 = 0x1.1107605230bc4p-7, SC_S3 = -0x1.994eb3774cf24p-13;
 
-MRP_HD const SinCosT& sincos_table(int k) {
-    // 2/pi * 2^24, pi/2, then the cos (c0..c4) and sin (s1..s3) minimax coefficients.
-    static constexpr SinCosT T0 = {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0,
-        0x1p0, -0x1.ffffffd0c621cp-2, 0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10, 0x1.99343027bf8c3p-16,
-        -0x1.555545995a603p-3, 0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13};
-    static constexpr SinCosT T1 = {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0,
-        -0x1p0, 0x1.ffffffd0c621cp-2, -0x1.55553e1068f19p-5, 0x1.6c087e89a359dp-10, -0x1.99343027bf8c3p-16,
-        -0x1.555545995a603p-3, 0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13};
-    return k ? T1 : T0;
-}
+MRP_HD double sc_sign(int n) { return ((n + 1) & 2) ? -1.0 : 1.0; }   // glibc sign[n & 3]
 
 MRP_HD uint32_t f2u(float f) { union { float f; uint32_t u; } x; x.f = f; return x.u; }
 MRP_HD float u2f(uint32_t u) { union { float f; uint32_t u; } x; x.u = u; return x.f; }
 MRP_HD uint32_t abstop12(float x) { return (f2u(x) >> 20) & 0x7ff; }
 
-MRP_HD float sincos_poly(double x, double x2, const SinCosT& p, int n) {
+// glibc sinf_poly; `neg` selects the second coefficient table (cos branch negated)
+MRP_HD float sincos_poly(double x, double x2, bool neg, int n) {
     if ((n & 1) == 0) {
         double x3 = x * x2;
-        double s1 = fma(x2, p.s3, p.s2);
+        double s1 = fma(x2, SC_S3, SC_S2);
         double x7 = x3 * x2;
-        double s = fma(x3, p.s1, x);
+        double s = fma(x3, SC_S1, x);
         return (float)fma(x7, s1, s);
     } else {
         double x4 = x2 * x2;
-        double c2 = fma(x2, p.c4, p.c3);
-        double c1 = fma(x2, p.c1, p.c0);
+        double c2 = fma(x2, SC_C4, SC_C3);
+        double c1 = fma(x2, SC_C1, SC_C0);
         double x6 = x4 * x2;
-        double c = fma(x4, p.c2, c1);
-        return (float)fma(x6, c2, c);
+        double c = fma(x4, SC_C2, c1);
+        float r = (float)fma(x6, c2, c);
+        return neg ? -r : r;   // fma/round-to-nearest are odd: negated coefficients negate exactly
     }
 }
 
-MRP_HD double reduce_fast(double x, const SinCosT& p, int* np) {
-    double r = x * p.hpi_inv;
+MRP_HD double reduce_fast(double x, int* np) {
+    double r = x * SC_HPI_INV;
     int n = ((int32_t)r + 0x800000) >> 24;
     *np = n;
-    return fma(-(double)n, p.hpi, x);
+    return fma(-(double)n, SC_HPI, x);
 }
 
 MRP_HD double reduce_large(uint32_t xi, int* np) {
@@ -127,18 +127,16 @@ MRP_HD float g_sinf(float y) {
     if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {
         s = x * x;
         if (abstop12(y) < abstop12(0x1p-12f)) return y;
-        return sincos_poly(x, s, sincos_table(0), 0);
+        return sincos_poly(x, s, false, 0);
     } else if (abstop12(y) < abstop12(120.0f)) {
-        x = reduce_fast(x, sincos_table(0), &n);
-        s = sincos_table(0).sign[n & 3];
-        const SinCosT& p = sincos_table((n & 2) ? 1 : 0);
-        return sincos_poly(x * s, x * x, p, n);
+        x = reduce_fast(x, &n);
+        s = sc_sign(n);
+        return sincos_poly(x * s, x * x, (n & 2) != 0, n);
     } else if (abstop12(y) < abstop12(__builtin_inff())) {
         uint32_t xi = f2u(y); int sign = xi >> 31;
         x = reduce_large(xi, &n);
-        s = sincos_table(0).sign[(n + sign) & 3];
-        const SinCosT& p = sincos_table(((n + sign) & 2) ? 1 : 0);
-        return sincos_poly(x * s, x * x, p, n);
+        s = sc_sign(n + sign);
+        return sincos_poly(x * s, x * x, ((n + sign) & 2) != 0, n);
     }
     return (y - y) / (y - y);
 }
@@ -148,18 +146,16 @@ MRP_HD float g_cosf(float y) {
     if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {
         double x2 = x * x;
         if (abstop12(y) < abstop12(0x1p-12f)) return 1.0f;
-        return sincos_poly(x, x2, sincos_table(0), 1);
+        return sincos_poly(x, x2, false, 1);
     } else if (abstop12(y) < abstop12(120.0f)) {
-        x = reduce_fast(x, sincos_table(0), &n);
-        s = sincos_table(0).sign[n & 3];
-        const SinCosT& p = sincos_table((n & 2) ? 1 : 0);
-        return sincos_poly(x * s, x * x, p, n ^ 1);
+        x = reduce_fast(x, &n);
+        s = sc_sign(n);
+        return sincos_poly(x * s, x * x, (n & 2) != 0, n ^ 1);
     } else if (abstop12(y) < abstop12(__builtin_inff())) {
         uint32_t xi = f2u(y); int sign = xi >> 31;
         x = reduce_large(xi, &n);
-        s = sincos_table(0).sign[(n + sign) & 3];
-        const SinCosT& p = sincos_table(((n + sign) & 2) ? 1 : 0);
-        return sincos_poly(x * s, x * x, p, n ^ 1);
+        s = sc_sign(n + sign);
+        return sincos_poly(x * s, x * x, ((n + sign) & 2) != 0, n ^ 1);
     }
     return (y - y) / (y - y);
 }

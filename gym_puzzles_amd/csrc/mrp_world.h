@@ -27,17 +27,25 @@ constexpr int NULLN = -1;
 // Diagnostic phase timing (build with -DMRP_STAMPS; never in the shipped build): thread 0 of
 // every lane accumulates s_memtime deltas per phase into g_stamps.
 #ifdef MRP_STAMPS
-__device__ unsigned long long g_stamps[16];
+__device__ unsigned long long g_stamps[16];     // per-phase sums over lane-steps
+__device__ unsigned long long g_pmax[16];       // per-phase max over lane-steps
+__device__ unsigned long long g_stepmax[256];   // per step (stepCounter mod 256): slowest lane's total
+__device__ unsigned long long g_rt[2];          // sums of lane totals: s_memtime ticks, s_memrealtime ticks
+__device__ uint32_t g_trace[16384][16];         // last step per lane: phases 0-10, total, nc, toi, pos, vel-units
+#define MRP_TRACE(k, v) do { if (tid == 0) sh.trace[k] += (v); } while (0)
 #define MRP_STAMP(k)                                                                        \
     do {                                                                                    \
         if (tid == 0) {                                                                     \
             unsigned long long _t = __builtin_amdgcn_s_memtime();                           \
             atomicAdd(&g_stamps[k], _t - sh.stamp_t);                                       \
+            atomicMax(&g_pmax[k], _t - sh.stamp_t);                                         \
+            sh.trace[k] += (uint32_t)(_t - sh.stamp_t);                                     \
             sh.stamp_t = _t;                                                                \
         }                                                                                   \
     } while (0)
 #else
 #define MRP_STAMP(k) do {} while (0)
+#define MRP_TRACE(k, v) do {} while (0)
 #endif
 constexpr float LINEAR_SLOP = 0.005f;
 constexpr float AABB_EXT = 0.1f;
@@ -174,7 +182,10 @@ template <int ENV> struct Shared {
     int done, kind;
     float act[D::ACT];
     double draws[D::NDRAW];
-    unsigned long long stamp_t;
+    unsigned long long stamp_t, stamp_t0, stamp_rt0;
+#ifdef MRP_STAMPS
+    uint32_t trace[16];
+#endif
 };
 
 template <int ENV> struct World {
@@ -922,6 +933,8 @@ template <int ENV> struct World {
                 is.pcx[i] = c.x; is.pcy[i] = c.y; is.pa[i] = 0.0f; is.vvx[i] = 0.0f; is.vvy[i] = 0.0f; is.vw[i] = 0.0f;
             }
         }
+        MRP_TRACE(12, is.nc);
+        MRP_TRACE(15, is.nc);
         if (is.nc > 0) {
             solver_init(is, vcs, pcs, true, dtRatio);
             solver_init_velocity(is, vcs, pcs);
@@ -1232,6 +1245,7 @@ template <int ENV> struct World {
             if (is_dyn(b)) { is.pcx[i] = S.cx[b]; is.pcy[i] = S.cy[b]; is.pa[i] = S.a[b]; is.vvx[i] = S.vx[b]; is.vvy[i] = S.vy[b]; is.vw[i] = S.w[b]; }
             else { V2 c = center(b); is.pcx[i] = c.x; is.pcy[i] = c.y; is.pa[i] = 0.0f; is.vvx[i] = 0.0f; is.vvy[i] = 0.0f; is.vw[i] = 0.0f; }
         }
+        MRP_TRACE(15, is.nc);
         solver_init(is, vcs, pcs, false, 1.0f);
         for (int i = 0; i < 20; ++i) if (solver_position(is, pcs, true, toiA, toiB)) break;
         {

@@ -121,6 +121,13 @@ int mrp_selftest_sincos(int device, const float* x, float* sin_out, float* cos_o
 /* Diagnostic builds (-DMRP_STAMPS) only: per-phase cycle totals of thread 0 since the last call
  * (returns MRP_E_STATE in the shipped build). */
 int mrp_debug_stamps(int device, uint64_t* out16);
+/* Diagnostic builds only: per-phase maxima over lane-steps, the slowest lane's total per step
+ * (256 slots, indexed by step counter mod 256) and the (s_memtime, s_memrealtime) sums of lane
+ * totals since the last call. */
+int mrp_debug_stamps_ext(int device, uint64_t* pmax16, uint64_t* stepmax256, uint64_t* rt2);
+/* Diagnostic builds only: the last step's per-lane trace, n_lanes x 16 words (phase cycles 0-10,
+ * total, island contacts, TOI events, position iterations, velocity-solver contact units). */
+int mrp_debug_trace(int device, uint32_t* out, int n_lanes);
 
 #ifdef __cplusplus
 }
