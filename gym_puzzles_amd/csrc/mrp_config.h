@@ -10,8 +10,8 @@
 namespace mrp {
 
 constexpr int MAX_POLY = 8;
-constexpr int TREE_N = 32;    // >= 2 * max proxies - 1 (15 proxies in the 3-block config)
-constexpr int MOVE_N = 32;
+constexpr int TREE_N = 32;    // largest dynamic-tree node pool (15 proxies in the 3-block config)
+constexpr int MOVE_N = 16;    // move buffer: at most NF (<= 15) proxies move between two UpdatePairs
 constexpr int MAXB = 9;       // bodies: <= 3 blocks + 5 agents ... + 4 walls (max over configs: 1 + 5 + 4 = 10)
 constexpr int MAXBODY = 10;
 constexpr int MAXF = 16;
@@ -26,6 +26,11 @@ template <> struct Dims<1> { static constexpr int V = 0, NA = 5, NB = 1, NF = 11
 template <> struct Dims<2> { static constexpr int V = 2, NA = 2, NB = 1, NF = 12, CMAX = 53, OBS = 39, ACT = 4, NDRAW = 7; };
 template <> struct Dims<3> { static constexpr int V = 2, NA = 2, NB = 1, NF = 12, CMAX = 53, OBS = 39, ACT = 4, NDRAW = 7; };
 template <> struct Dims<4> { static constexpr int V = 2, NA = 2, NB = 3, NF = 15, CMAX = 91, OBS = 69, ACT = 4, NDRAW = 9; };
+
+// Node pool of a lane's dynamic tree.  b2DynamicTree starts at 16 nodes and doubles only when
+// all are live; a world holds at most 2 * proxies - 1 live nodes, so an env with <= 8 proxies
+// never grows past 16 and its node ids (free-list order) never exceed 15.
+template <int ENV> constexpr int tree_n() { return 2 * Dims<ENV>::NF - 1 <= 16 ? 16 : 32; }
 
 struct ShapeDef {
     int count;

@@ -33,7 +33,8 @@ template <int ENV> struct Env : World<ENV> {
     __device__ __forceinline__ Env(typename W::SH& s, const EnvTables& t, const EnvParams& p, int thread) : W(s, t, p, thread) {}
 
     __device__ __forceinline__ void init_empty_world() {   // fresh b2World (Box2D.b2World(gravity=(0,0), doSleep=False))
-        for (int i = 0; i < TREE_N; ++i) { S.tpar[i] = i + 1 < TREE_N ? i + 1 : NULLN; S.th[i] = -1; S.tud[i] = -1; S.tc1[i] = NULLN; S.tc2[i] = NULLN; }
+        constexpr int TN = W::LS::TN;
+        for (int i = 0; i < TN; ++i) { S.tpar[i] = i + 1 < TN ? i + 1 : NULLN; S.th[i] = -1; S.tud[i] = -1; S.tc1[i] = NULLN; S.tc2[i] = NULLN; }
         S.root = NULLN; S.freeList = 0; S.nodeCount = 0; S.moveCount = 0;
         S.cHead = NULLN; S.cFree = 0; S.cCount = 0;
         for (int c = 0; c < D::CMAX; ++c) S.cnext[c] = c + 1 < D::CMAX ? c + 1 : NULLN;

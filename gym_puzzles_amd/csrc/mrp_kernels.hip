@@ -48,6 +48,28 @@ __device__ __forceinline__ void store_state(const LaneState<ENV>& S, uint32_t* _
     for (int i = tid; i < NW; i += BLOCK) dst[i] = w[i];
 }
 
+// copy this env's hot tables from __constant__ memory into the lane's LDS (before the
+// barrier that follows load_state)
+template <int ENV>
+__device__ __forceinline__ void load_tables(LdsTables<ENV>& L, int tid) {
+    using LT = LdsTables<ENV>;
+    const EnvTables& T = g_tables[ENV];
+    constexpr int SW = LT::NF * (int)(sizeof(ShapeDef) / 4);
+    const word_t* src = reinterpret_cast<const word_t*>(T.shape);
+    word_t* dst = reinterpret_cast<word_t*>(L.shape);
+    for (int i = tid; i < SW; i += BLOCK) dst[i] = src[i];
+    if (tid < LT::NF) {
+        L.fix_body[tid] = T.fix_body[tid]; L.fix_friction[tid] = T.fix_friction[tid];
+        L.fix_restitution[tid] = T.fix_restitution[tid];
+    }
+    if (tid < LT::NBODY) {
+        L.invMass[tid] = T.invMass[tid]; L.invI[tid] = T.invI[tid]; L.lcx[tid] = T.lcx[tid]; L.lcy[tid] = T.lcy[tid];
+        L.linDamp[tid] = T.linDamp[tid]; L.angDamp[tid] = T.angDamp[tid];
+        L.body_fix0[tid] = T.body_fix0[tid]; L.body_nfix[tid] = T.body_nfix[tid];
+    }
+    if (tid < 4) { L.wall_px[tid] = T.wall_px[tid]; L.wall_py[tid] = T.wall_py[tid]; }
+}
+
 template <int ENV>
 __global__ __launch_bounds__(BLOCK) void k_init(uint32_t* state, int nl) {
     __shared__ Shared<ENV> sh;
@@ -93,6 +115,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_reset(uint32_t* state, int nl, con
     if (lane >= nl) return;
     if (mask && !mask[lane]) return;
     load_state<ENV>(sh.S, state, lane, tid);
+    load_tables<ENV>(sh.lt, tid);
     __syncthreads();
     stage_reset_inputs<ENV>(sh, draws, actions, lane, tid, seed, lane_offset + lane);
     Env<ENV> e(sh, g_tables[ENV], P, tid);
@@ -118,6 +141,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_step(uint32_t* state, int nl, cons
     long long toi0 = 0, pos0 = 0;
 #endif
     load_state<ENV>(sh.S, state, lane, tid);
+    load_tables<ENV>(sh.lt, tid);
     __syncthreads();
 #ifdef MRP_STAMPS
     toi0 = sh.S.toiEvents; pos0 = sh.S.posIters;

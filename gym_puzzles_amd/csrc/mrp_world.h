@@ -72,6 +72,8 @@ template <int ENV> struct LaneState {
     using D = Dims<ENV>;
     static constexpr int ND = D::NA + D::NB;
     static constexpr int C = D::CMAX;
+    static constexpr int TN = tree_n<ENV>();
+    static_assert(D::NF < MOVE_N, "move buffer smaller than the proxy count");
     // dynamic bodies (blocks, then agents): transform, sweep, velocity, force accumulators
     float xpx[ND], xpy[ND], xs[ND], xc[ND];
     float c0x[ND], c0y[ND], cx[ND], cy[ND], a0[ND], a[ND], alpha0[ND];
@@ -80,8 +82,8 @@ template <int ENV> struct LaneState {
     // fixtures -> broad-phase proxy id
     int proxy[D::NF];
     // dynamic AABB tree (fat AABBs)
-    float tlx[TREE_N], tly[TREE_N], thx[TREE_N], thy[TREE_N];
-    int tpar[TREE_N], tc1[TREE_N], tc2[TREE_N], th[TREE_N], tud[TREE_N];
+    float tlx[TN], tly[TN], thx[TN], thy[TN];
+    int tpar[TN], tc1[TN], tc2[TN], th[TN], tud[TN];
     int root, freeList, nodeCount, moveCount;
     int moveBuf[MOVE_N];
     // contacts (slot pool + creation-descending doubly linked list)
@@ -116,10 +118,10 @@ struct VC {
     float mA, mB, iA, iB, friction, restitution;
     int iaI, ibI, pointCount, slot;
 };
-struct PC {
+struct PC {   // position constraint; body indices and mass data are read from the contact's VC
     float lpx[2], lpy[2], lnx, lny, lpx0, lpy0;
-    float mA, mB, iA, iB, lcAx, lcAy, lcBx, lcBy, rA, rB;
-    int iaI, ibI, type, pointCount;
+    float lcAx, lcAy, lcBx, lcBy, rA, rB;
+    int type, pointCount;
 };
 template <int NBODY, int C> struct IslT {
     int bodies[NBODY];
@@ -135,14 +137,31 @@ struct Simplex { SVert v[3]; int count; };
 struct SCache { float metric; int count; int iA[3], iB[3]; };
 struct SepFn { int type; V2 lp, axis; };
 
+// Per-launch LDS copy of the env tables the step indexes with lane-varying indices (fixture
+// shapes, fixture -> body, per-body mass and damping, wall poses).  From __constant__ memory
+// those reads are vector-memory loads whose divergent addresses serialise in the texture path
+// (the parallel narrow phase and TOI give every thread its own contact); from LDS they are
+// ds_read at LDS latency.
+template <int ENV> struct LdsTables {
+    static constexpr int NF = Dims<ENV>::NF, NBODY = Dims<ENV>::NA + Dims<ENV>::NB + 4;
+    ShapeDef shape[NF];
+    int fix_body[NF];
+    float fix_friction[NF], fix_restitution[NF];
+    float invMass[NBODY], invI[NBODY], lcx[NBODY], lcy[NBODY], linDamp[NBODY], angDamp[NBODY];
+    int body_fix0[NBODY], body_nfix[NBODY];
+    float wall_px[4], wall_py[4];
+};
+
 // Per-lane LDS working set of the cooperative (one wave per world) step.
 template <int ENV> struct Shared {
     using D = Dims<ENV>;
     using LS = LaneState<ENV>;
     static constexpr int ND = LS::ND, NBODY = ND + 4, C = D::CMAX;
     LS S;
+    LdsTables<ENV> lt;
     IslT<NBODY, C> isl;
     int stack[NBODY];
+    int isl_go;
     float salpha0[4];
     // collide: contact list snapshot (the per-contact manifolds live in the phase union below)
     int clist[C];
@@ -155,7 +174,7 @@ template <int ENV> struct Shared {
     // broad phase: active proxy ids (ascending)
     int nprox;
     uint32_t moved;
-    int prox[TREE_N];
+    int prox[LS::TN];
     // TOI scan bookkeeping
     int tn, np, toi_done, toi_fnc;
     int tcand[C];
@@ -173,7 +192,7 @@ template <int ENV> struct Shared {
             float tpx[2][C], tpy[2][C];
             uint32_t tmid[2][C];
         } col;
-        uint8_t pover[TREE_N * (TREE_N - 1) / 2];
+        uint8_t pover[LS::TN * (LS::TN - 1) / 2];
         struct { SweepV tsA[C], tsB[C]; TOIOut tout[C]; } toi;
     } u;
     // env I/O
@@ -197,22 +216,23 @@ template <int ENV> struct World {
     using Isl = IslT<NBODY, C>;
     SH& sh;
     LS& S;
+    const LdsTables<ENV>& L;
     const EnvTables& T;
     const EnvParams& P;
     const int tid;
 
-    __device__ __forceinline__ World(SH& s, const EnvTables& t, const EnvParams& p, int thread) : sh(s), S(s.S), T(t), P(p), tid(thread) {}
+    __device__ __forceinline__ World(SH& s, const EnvTables& t, const EnvParams& p, int thread) : sh(s), S(s.S), L(s.lt), T(t), P(p), tid(thread) {}
 
     // ------------------------------------------------------------------ bodies
     __device__ __forceinline__ bool is_dyn(int b) const { return b < ND; }
     __device__ __forceinline__ Xf xf(int b) const {
         Xf r;
         if (b < ND) { r.p = v2(S.xpx[b], S.xpy[b]); r.q.s = S.xs[b]; r.q.c = S.xc[b]; }
-        else { r.p = v2(T.wall_px[b - ND], T.wall_py[b - ND]); r.q.s = 0.0f; r.q.c = 1.0f; }
+        else { r.p = v2(L.wall_px[b - ND], L.wall_py[b - ND]); r.q.s = 0.0f; r.q.c = 1.0f; }
         return r;
     }
-    __device__ __forceinline__ V2 center(int b) const { return b < ND ? v2(S.cx[b], S.cy[b]) : v2(T.wall_px[b - ND], T.wall_py[b - ND]); }
-    __device__ __forceinline__ V2 lc(int b) const { return v2(T.lcx[b], T.lcy[b]); }
+    __device__ __forceinline__ V2 center(int b) const { return b < ND ? v2(S.cx[b], S.cy[b]) : v2(L.wall_px[b - ND], L.wall_py[b - ND]); }
+    __device__ __forceinline__ V2 lc(int b) const { return v2(L.lcx[b], L.lcy[b]); }
     __device__ __forceinline__ void sync_transform(int b) {   // b2Body::SynchronizeTransform
         Rot q = rot(S.a[b]);
         S.xs[b] = q.s; S.xc[b] = q.c;
@@ -352,7 +372,7 @@ template <int ENV> struct World {
     }
     __device__ __forceinline__ void create_proxy(int f, Xf x) {
         float lx, ly, hx, hy;
-        poly_aabb(T.shape[f], x, lx, ly, hx, hy);
+        poly_aabb(L.shape[f], x, lx, ly, hx, hy);
         int id = t_alloc();
         S.tlx[id] = lx - AABB_EXT; S.tly[id] = ly - AABB_EXT; S.thx[id] = hx + AABB_EXT; S.thy[id] = hy + AABB_EXT;
         S.tud[id] = f; S.th[id] = 0;
@@ -388,11 +408,11 @@ template <int ENV> struct World {
         Xf x1; x1.q = rot(S.a0[b]);
         x1.p = vsub(v2(S.c0x[b], S.c0y[b]), mul_rv(x1.q, lc(b)));
         Xf x2 = xf(b);
-        for (int k = T.body_nfix[b] - 1; k >= 0; --k) {
-            int f = T.body_fix0[b] + k;
+        for (int k = L.body_nfix[b] - 1; k >= 0; --k) {
+            int f = L.body_fix0[b] + k;
             float l1x, l1y, h1x, h1y, l2x, l2y, h2x, h2y;
-            poly_aabb(T.shape[f], x1, l1x, l1y, h1x, h1y);
-            poly_aabb(T.shape[f], x2, l2x, l2y, h2x, h2y);
+            poly_aabb(L.shape[f], x1, l1x, l1y, h1x, h1y);
+            poly_aabb(L.shape[f], x2, l2x, l2y, h2x, h2y);
             V2 disp = vsub(x2.p, x1.p);
             move_proxy(S.proxy[f], fmin_(l1x, l2x), fmin_(l1y, l2y), fmax_(h1x, h2x), fmax_(h1y, h2y), disp);
         }
@@ -400,7 +420,7 @@ template <int ENV> struct World {
 
     // ------------------------------------------------------------------ contacts
     __device__ __forceinline__ void contact_event(int c, int value) {   // ContactDetector (multi_robot_puzzle_00.py:92-111)
-        int bA = T.fix_body[S.cfa[c]], bB = T.fix_body[S.cfb[c]];
+        int bA = L.fix_body[S.cfa[c]], bB = L.fix_body[S.cfb[c]];
         for (int i = 0; i < NA; ++i) {
             int ag = NB + i;
             if (ag == bA || ag == bB) {
@@ -410,7 +430,7 @@ template <int ENV> struct World {
         }
     }
     __device__ __forceinline__ void add_pair(int fa, int fb) {   // b2ContactManager::AddPair
-        int bA = T.fix_body[fa], bB = T.fix_body[fb];
+        int bA = L.fix_body[fa], bB = L.fix_body[fb];
         if (bA == bB) return;
         for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
             if ((S.cfa[c] == fa && S.cfb[c] == fb) || (S.cfa[c] == fb && S.cfb[c] == fa)) return;
@@ -419,7 +439,7 @@ template <int ENV> struct World {
         int c = S.cFree;
         S.cFree = S.cnext[c];
         S.cfa[c] = fa; S.cfb[c] = fb; S.cflags[c] = CF_ENABLED; S.ctoiCount[c] = 0; S.ctoi[c] = 1.0f;
-        S.cfric[c] = sqrtf(T.fix_friction[fa] * T.fix_friction[fb]);
+        S.cfric[c] = sqrtf(L.fix_friction[fa] * L.fix_friction[fb]);
         S.mpc[c] = 0;
         S.cprev[c] = NULLN; S.cnext[c] = S.cHead;
         if (S.cHead != NULLN) S.cprev[S.cHead] = c;
@@ -446,7 +466,7 @@ template <int ENV> struct World {
             S.moveCount = 0;
             int n = 0;
             if (moved)
-                for (int a = 0; a < TREE_N; ++a) if (S.tud[a] >= 0 && t_leaf(a)) sh.prox[n++] = a;
+                for (int a = 0; a < LS::TN; ++a) if (S.tud[a] >= 0 && t_leaf(a)) sh.prox[n++] = a;
             sh.nprox = n;
             sh.moved = moved;
         }
@@ -604,7 +624,7 @@ template <int ENV> struct World {
     // b2Contact::Update on one contact (serial callers: TOI)
     __device__ __forceinline__ void contact_update(int c) {
         int fa = S.cfa[c], fb = S.cfb[c];
-        collide_polygons(-1, T.shape[fa], xf(T.fix_body[fa]), T.shape[fb], xf(T.fix_body[fb]));
+        collide_polygons(-1, L.shape[fa], xf(L.fix_body[fa]), L.shape[fb], xf(L.fix_body[fb]));
         contact_commit(c, -1);
     }
     // b2ContactManager::Collide.  Cooperative: thread 0 snapshots the contact list, all threads
@@ -623,7 +643,7 @@ template <int ENV> struct World {
             int fa = S.cfa[c], fb = S.cfb[c];
             bool ov = fat_overlap(S.proxy[fa], S.proxy[fb]);
             sh.cover[i] = ov ? 1 : 0;
-            if (ov) collide_polygons(i, T.shape[fa], xf(T.fix_body[fa]), T.shape[fb], xf(T.fix_body[fb]));
+            if (ov) collide_polygons(i, L.shape[fa], xf(L.fix_body[fa]), L.shape[fb], xf(L.fix_body[fb]));
         }
         __syncthreads();
         if (tid == 0) {
@@ -637,27 +657,25 @@ template <int ENV> struct World {
     }
 
     // ---------------------------------------------------------------- contact solver
-    __device__ __forceinline__ float body_invMass(int b) const { return T.invMass[b]; }
-    __device__ __forceinline__ float body_invI(int b) const { return T.invI[b]; }
+    __device__ __forceinline__ float body_invMass(int b) const { return L.invMass[b]; }
+    __device__ __forceinline__ float body_invI(int b) const { return L.invI[b]; }
 
     __device__ __forceinline__ void solver_init(Isl& is, VC* vcs, PC* pcs, bool warm, float dtRatio) {
         for (int i = 0; i < is.nc; ++i) {
             int c = is.contacts[i];
             int fa = S.cfa[c], fb = S.cfb[c];
-            int bA = T.fix_body[fa], bB = T.fix_body[fb];
+            int bA = L.fix_body[fa], bB = L.fix_body[fb];
             int pcount = S.mpc[c];
             VC& vc = vcs[i];
-            vc.friction = S.cfric[c]; vc.restitution = fmax_(T.fix_restitution[fa], T.fix_restitution[fb]);
+            vc.friction = S.cfric[c]; vc.restitution = fmax_(L.fix_restitution[fa], L.fix_restitution[fb]);
             vc.iaI = is.index[bA]; vc.ibI = is.index[bB];
-            vc.mA = T.invMass[bA]; vc.mB = T.invMass[bB]; vc.iA = T.invI[bA]; vc.iB = T.invI[bB];
+            vc.mA = L.invMass[bA]; vc.mB = L.invMass[bB]; vc.iA = L.invI[bA]; vc.iB = L.invI[bB];
             vc.slot = c; vc.pointCount = pcount;
             vc.k0 = vc.k1 = vc.k2 = vc.k3 = 0.0f; vc.nm0 = vc.nm1 = vc.nm2 = vc.nm3 = 0.0f;
             PC& pc = pcs[i];
-            pc.iaI = vc.iaI; pc.ibI = vc.ibI;
-            pc.mA = vc.mA; pc.mB = vc.mB; pc.iA = vc.iA; pc.iB = vc.iB;
-            pc.lcAx = T.lcx[bA]; pc.lcAy = T.lcy[bA]; pc.lcBx = T.lcx[bB]; pc.lcBy = T.lcy[bB];
+            pc.lcAx = L.lcx[bA]; pc.lcAy = L.lcy[bA]; pc.lcBx = L.lcx[bB]; pc.lcBy = L.lcy[bB];
             pc.lnx = S.mlnx[c]; pc.lny = S.mlny[c]; pc.lpx0 = S.mlpx[c]; pc.lpy0 = S.mlpy[c];
-            pc.pointCount = pcount; pc.rA = T.shape[fa].radius; pc.rB = T.shape[fb].radius; pc.type = S.mtype[c];
+            pc.pointCount = pcount; pc.rA = L.shape[fa].radius; pc.rB = L.shape[fb].radius; pc.type = S.mtype[c];
             for (int j = 0; j < pcount; ++j) {
                 if (warm) { vc.ni[j] = dtRatio * S.mni[j][c]; vc.ti[j] = dtRatio * S.mti[j][c]; }
                 else { vc.ni[j] = 0.0f; vc.ti[j] = 0.0f; }
@@ -841,16 +859,17 @@ template <int ENV> struct World {
             for (int j = 0; j < vc.pointCount; ++j) { S.mni[j][vc.slot] = vc.ni[j]; S.mti[j][vc.slot] = vc.ti[j]; }
         }
     }
-    __device__ __forceinline__ bool solver_position(Isl& is, PC* pcs, bool toi, int toiA, int toiB) {
+    __device__ __forceinline__ bool solver_position(Isl& is, const VC* vcs, PC* pcs, bool toi, int toiA, int toiB) {
         float minSep = 0.0f;
         for (int i = 0; i < is.nc; ++i) {
             PC& pc = pcs[i];
-            int ia = pc.iaI, ib = pc.ibI;
+            const VC& vc = vcs[i];
+            int ia = vc.iaI, ib = vc.ibI;
             float mA, iA, mB, iB;
-            if (!toi) { mA = pc.mA; iA = pc.iA; mB = pc.mB; iB = pc.iB; }
+            if (!toi) { mA = vc.mA; iA = vc.iA; mB = vc.mB; iB = vc.iB; }
             else {
-                mA = 0.0f; iA = 0.0f; if (ia == toiA || ia == toiB) { mA = pc.mA; iA = pc.iA; }
-                mB = 0.0f; iB = 0.0f; if (ib == toiA || ib == toiB) { mB = pc.mB; iB = pc.iB; }
+                mA = 0.0f; iA = 0.0f; if (ia == toiA || ia == toiB) { mA = vc.mA; iA = vc.iA; }
+                mB = 0.0f; iB = 0.0f; if (ib == toiA || ib == toiB) { mB = vc.mB; iB = vc.iB; }
             }
             V2 cA = v2(is.pcx[ia], is.pcy[ia]); float aA = is.pa[ia];
             V2 cB = v2(is.pcx[ib], is.pcy[ib]); float aB = is.pa[ib];
@@ -891,6 +910,133 @@ template <int ENV> struct World {
         }
         return toi ? (minSep >= -1.5f * LINEAR_SLOP) : (minSep >= -3.0f * LINEAR_SLOP);
     }
+    // ---------------------------------------------------------------- lane-distributed velocity sweeps
+    // b2ContactSolver::SolveVelocityConstraints x `iters` with the island's constraint data held
+    // in VGPRs across the wave: contact i's constants and impulses in lane i, island body k's
+    // velocity in lane k.  The Gauss-Seidel order is unchanged (one contact after another); each
+    // contact reads its operands with v_readlane and writes results back with a lane select, so the
+    // iters x nc contact updates never wait on LDS.  Float operations and their order are those
+    // of solver_velocity, so the result is bitwise identical.  Every thread of the wave calls it;
+    // needs is.nc <= 64.
+    __device__ __forceinline__ static float rdl(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+    __device__ __forceinline__ static int rdli(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+    // lane l of `old` replaced by the (wave-uniform) x: one v_cmp + v_cndmask
+    __device__ __forceinline__ float wrl(float old, float x, int l) const { return tid == l ? x : old; }
+    __device__ __forceinline__ void solver_velocity_lanes(Isl& is, VC* vcs, int iters) {
+        const int nc = is.nc;
+        const VC& my = vcs[tid < nc ? tid : 0];
+        const float rAx0 = my.rAx[0], rAy0 = my.rAy[0], rBx0 = my.rBx[0], rBy0 = my.rBy[0];
+        const float rAx1 = my.rAx[1], rAy1 = my.rAy[1], rBx1 = my.rBx[1], rBy1 = my.rBy[1];
+        const float nmass0 = my.nmass[0], nmass1 = my.nmass[1], tmass0 = my.tmass[0], tmass1 = my.tmass[1];
+        const float vbias0 = my.vbias[0], vbias1 = my.vbias[1];
+        const float cnx = my.nx, cny = my.ny, k0 = my.k0, k1 = my.k1, k2 = my.k2, k3 = my.k3;
+        const float nm0 = my.nm0, nm1 = my.nm1, nm2 = my.nm2, nm3 = my.nm3;
+        const float cmA = my.mA, cmB = my.mB, ciA = my.iA, ciB = my.iB, cfr = my.friction;
+        const int cia = my.iaI, cib = my.ibI, cpc = my.pointCount;
+        float ni0 = my.ni[0], ni1 = my.ni[1], ti0 = my.ti[0], ti1 = my.ti[1];
+        const int bk = tid < is.nb ? tid : 0;
+        float bvx = is.vvx[bk], bvy = is.vvy[bk], bw = is.vw[bk];
+        for (int it = 0; it < iters; ++it) {
+            for (int i = 0; i < nc; ++i) {
+                const int ia = rdli(cia, i), ib = rdli(cib, i), pcount = rdli(cpc, i);
+                const float mA = rdl(cmA, i), iA = rdl(ciA, i), mB = rdl(cmB, i), iB = rdl(ciB, i);
+                V2 vA = v2(rdl(bvx, ia), rdl(bvy, ia)); float wA = rdl(bw, ia);
+                V2 vB = v2(rdl(bvx, ib), rdl(bvy, ib)); float wB = rdl(bw, ib);
+                V2 normal = v2(rdl(cnx, i), rdl(cny, i)), tangent = vcross_vs(normal, 1.0f);
+                const float friction = rdl(cfr, i);
+                {   // friction, point 0
+                    V2 rA = v2(rdl(rAx0, i), rdl(rAy0, i)), rB = v2(rdl(rBx0, i), rdl(rBy0, i));
+                    V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
+                    float vt = vdot(dv, tangent) - 0.0f;
+                    float lambda = rdl(tmass0, i) * (-vt);
+                    float maxFriction = friction * rdl(ni0, i);
+                    float told = rdl(ti0, i);
+                    float newImpulse = fclamp(told + lambda, -maxFriction, maxFriction);
+                    lambda = newImpulse - told;
+                    ti0 = wrl(ti0, newImpulse, i);
+                    V2 P = vmul(lambda, tangent);
+                    vA = vsub(vA, vmul(mA, P));
+                    wA -= iA * vcross(rA, P);
+                    vB = vadd(vB, vmul(mB, P));
+                    wB += iB * vcross(rB, P);
+                }
+                if (pcount == 2) {   // friction, point 1
+                    V2 rA = v2(rdl(rAx1, i), rdl(rAy1, i)), rB = v2(rdl(rBx1, i), rdl(rBy1, i));
+                    V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
+                    float vt = vdot(dv, tangent) - 0.0f;
+                    float lambda = rdl(tmass1, i) * (-vt);
+                    float maxFriction = friction * rdl(ni1, i);
+                    float told = rdl(ti1, i);
+                    float newImpulse = fclamp(told + lambda, -maxFriction, maxFriction);
+                    lambda = newImpulse - told;
+                    ti1 = wrl(ti1, newImpulse, i);
+                    V2 P = vmul(lambda, tangent);
+                    vA = vsub(vA, vmul(mA, P));
+                    wA -= iA * vcross(rA, P);
+                    vB = vadd(vB, vmul(mB, P));
+                    wB += iB * vcross(rB, P);
+                }
+                if (pcount == 1) {
+                    V2 rA = v2(rdl(rAx0, i), rdl(rAy0, i)), rB = v2(rdl(rBx0, i), rdl(rBy0, i));
+                    V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
+                    float vn = vdot(dv, normal);
+                    float nold = rdl(ni0, i);
+                    float lambda = -rdl(nmass0, i) * (vn - rdl(vbias0, i));
+                    float newImpulse = fmax_(nold + lambda, 0.0f);
+                    lambda = newImpulse - nold;
+                    ni0 = wrl(ni0, newImpulse, i);
+                    V2 P = vmul(lambda, normal);
+                    vA = vsub(vA, vmul(mA, P));
+                    wA -= iA * vcross(rA, P);
+                    vB = vadd(vB, vmul(mB, P));
+                    wB += iB * vcross(rB, P);
+                } else {
+                    V2 r1A = v2(rdl(rAx0, i), rdl(rAy0, i)), r1B = v2(rdl(rBx0, i), rdl(rBy0, i));
+                    V2 r2A = v2(rdl(rAx1, i), rdl(rAy1, i)), r2B = v2(rdl(rBx1, i), rdl(rBy1, i));
+                    const float K0 = rdl(k0, i), K1 = rdl(k1, i), K2 = rdl(k2, i), K3 = rdl(k3, i);
+                    const float M0 = rdl(nm0, i), M1 = rdl(nm1, i), M2 = rdl(nm2, i), M3 = rdl(nm3, i);
+                    V2 a = v2(rdl(ni0, i), rdl(ni1, i));
+                    V2 dv1 = vsub(vsub(vadd(vB, vcross_sv(wB, r1B)), vA), vcross_sv(wA, r1A));
+                    V2 dv2 = vsub(vsub(vadd(vB, vcross_sv(wB, r2B)), vA), vcross_sv(wA, r2A));
+                    float vn1 = vdot(dv1, normal), vn2 = vdot(dv2, normal);
+                    V2 b = v2(vn1 - rdl(vbias0, i), vn2 - rdl(vbias1, i));
+                    b = vsub(b, v2(K0 * a.x + K2 * a.y, K1 * a.x + K3 * a.y));
+                    V2 x;
+                    bool ok = false;
+                    x = vneg(v2(M0 * b.x + M2 * b.y, M1 * b.x + M3 * b.y));
+                    if (x.x >= 0.0f && x.y >= 0.0f) ok = true;
+                    if (!ok) {
+                        x.x = -rdl(nmass0, i) * b.x; x.y = 0.0f;
+                        vn2 = K1 * x.x + b.y;
+                        if (x.x >= 0.0f && vn2 >= 0.0f) ok = true;
+                    }
+                    if (!ok) {
+                        x.x = 0.0f; x.y = -rdl(nmass1, i) * b.y;
+                        vn1 = K2 * x.y + b.x;
+                        if (x.y >= 0.0f && vn1 >= 0.0f) ok = true;
+                    }
+                    if (!ok) {
+                        x.x = 0.0f; x.y = 0.0f; vn1 = b.x; vn2 = b.y;
+                        if (vn1 >= 0.0f && vn2 >= 0.0f) ok = true;
+                    }
+                    if (ok) {
+                        V2 d = vsub(x, a);
+                        V2 P1 = vmul(d.x, normal), P2 = vmul(d.y, normal);
+                        vA = vsub(vA, vmul(mA, vadd(P1, P2)));
+                        wA -= iA * (vcross(r1A, P1) + vcross(r2A, P2));
+                        vB = vadd(vB, vmul(mB, vadd(P1, P2)));
+                        wB += iB * (vcross(r1B, P1) + vcross(r2B, P2));
+                        ni0 = wrl(ni0, x.x, i); ni1 = wrl(ni1, x.y, i);
+                    }
+                }
+                bvx = wrl(bvx, vA.x, ia); bvy = wrl(bvy, vA.y, ia); bw = wrl(bw, wA, ia);
+                bvx = wrl(bvx, vB.x, ib); bvy = wrl(bvy, vB.y, ib); bw = wrl(bw, wB, ib);
+            }
+        }
+        if (tid < is.nb) { is.vvx[tid] = bvx; is.vvy[tid] = bvy; is.vw[tid] = bw; }
+        if (tid < nc) { VC& o = vcs[tid]; o.ni[0] = ni0; o.ni[1] = ni1; o.ti[0] = ti0; o.ti[1] = ti1; }
+    }
+
     __device__ __forceinline__ void integrate_positions(Isl& is, float h) {
         for (int i = 0; i < is.nb; ++i) {
             V2 c = v2(is.pcx[i], is.pcy[i]); float a = is.pa[i];
@@ -913,8 +1059,10 @@ template <int ENV> struct World {
     }
     __device__ __forceinline__ void island_add_body(Isl& is, int b) { is.index[b] = is.nb; is.bodies[is.nb++] = b; }
 
-    // b2Island::Solve (discrete step of one island)
-    __device__ __forceinline__ void island_solve(Isl& is, float h, float dtRatio, VC* vcs, PC* pcs) {
+    // b2Island::Solve (discrete step of one island), in three parts: island_pre and island_post
+    // run on thread 0; the velocity iterations between them run on the whole wave
+    // (solver_velocity_lanes), or on thread 0 over LDS when the island has more than 64 contacts.
+    __device__ __forceinline__ void island_pre(Isl& is, float h, float dtRatio, VC* vcs, PC* pcs) {
         for (int i = 0; i < is.nb; ++i) {
             int b = is.bodies[i];
             if (is_dyn(b)) {
@@ -922,11 +1070,11 @@ template <int ENV> struct World {
                 V2 v = v2(S.vx[b], S.vy[b]); float w = S.w[b];
                 S.c0x[b] = S.cx[b]; S.c0y[b] = S.cy[b]; S.a0[b] = S.a[b];
                 V2 g = v2(1.0f * 0.0f, 1.0f * 0.0f);   // gravityScale * gravity (0,0)
-                V2 acc = vadd(g, vmul(T.invMass[b], v2(S.fx[b], S.fy[b])));
+                V2 acc = vadd(g, vmul(L.invMass[b], v2(S.fx[b], S.fy[b])));
                 v = vadd(v, vmul(h, acc));
-                w += h * T.invI[b] * S.tq[b];
-                { float s = 1.0f / (1.0f + h * T.linDamp[b]); v.x *= s; v.y *= s; }
-                w *= 1.0f / (1.0f + h * T.angDamp[b]);
+                w += h * L.invI[b] * S.tq[b];
+                { float s = 1.0f / (1.0f + h * L.linDamp[b]); v.x *= s; v.y *= s; }
+                w *= 1.0f / (1.0f + h * L.angDamp[b]);
                 is.pcx[i] = c.x; is.pcy[i] = c.y; is.pa[i] = a; is.vvx[i] = v.x; is.vvy[i] = v.y; is.vw[i] = w;
             } else {
                 V2 c = center(b);
@@ -934,19 +1082,20 @@ template <int ENV> struct World {
             }
         }
         MRP_TRACE(12, is.nc);
-        MRP_TRACE(15, is.nc);
         if (is.nc > 0) {
+            MRP_TRACE(15, 1);
             solver_init(is, vcs, pcs, true, dtRatio);
             solver_init_velocity(is, vcs, pcs);
             solver_warm_start(is, vcs);
-            for (int it = 0; it < 180; ++it) solver_velocity(is, vcs);
-            solver_store(is, vcs);
         }
+    }
+    __device__ __forceinline__ void island_post(Isl& is, float h, VC* vcs, PC* pcs) {
+        if (is.nc > 0) solver_store(is, vcs);
         integrate_positions(is, h);
         if (is.nc > 0) {
             for (int it = 0; it < 60; ++it) {
                 ++S.posIters;
-                if (solver_position(is, pcs, false, -1, -1)) break;
+                if (solver_position(is, vcs, pcs, false, -1, -1)) break;
             }
         } else {
             ++S.posIters;   // an empty island's first position pass already reports solved
@@ -960,46 +1109,64 @@ template <int ENV> struct World {
         }
     }
 
-    // b2World::Solve, serial part (thread 0): island DFS + island solves + SynchronizeFixtures.
-    // The trailing FindNewContacts is cooperative and issued by world_step_coop.
-    __device__ __forceinline__ void solve_serial(float h, float dtRatio) {
+    // b2World::Solve, cooperative (every thread of the wave calls it): thread 0 builds one island
+    // at a time by DFS (body list = reverse creation order; contact edges in list order) and runs
+    // its serial parts; the wave runs its velocity iterations.  Islands are solved in the
+    // reference's order.  The trailing FindNewContacts is issued by world_step_coop.
+    __device__ __forceinline__ void solve_coop(float h, float dtRatio) {
         Isl& is = sh.isl;
-        uint32_t bflag = 0;   // body island flags (bit per body)
-        for (int c = S.cHead; c != NULLN; c = S.cnext[c]) S.cflags[c] &= ~CF_ISLAND;
-        int* stack = sh.stack;
-        // body list = reverse creation order: walls (static, never seeds), agents, blocks
-        for (int seed = ND - 1; seed >= 0; --seed) {
-            if (bflag & (1u << seed)) continue;
-            is.nb = 0; is.nc = 0;
-            int sc = 0;
-            stack[sc++] = seed; bflag |= 1u << seed;
-            while (sc > 0) {
-                int b = stack[--sc];
-                island_add_body(is, b);
-                if (!is_dyn(b)) continue;
-                for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
-                    int bA = T.fix_body[S.cfa[c]], bB = T.fix_body[S.cfb[c]];
-                    if (bA != b && bB != b) continue;
-                    if (S.cflags[c] & CF_ISLAND) continue;
-                    if ((S.cflags[c] & CF_ENABLED) == 0 || (S.cflags[c] & CF_TOUCHING) == 0) continue;
-                    is.contacts[is.nc++] = c;
-                    S.cflags[c] |= CF_ISLAND;
-                    int other = bA == b ? bB : bA;
-                    if (bflag & (1u << other)) continue;
-                    stack[sc++] = other; bflag |= 1u << other;
+        uint32_t bflag = 0;   // body island flags (bit per body), thread 0
+        int seed = ND - 1;    // next DFS seed, thread 0
+        if (tid == 0) for (int c = S.cHead; c != NULLN; c = S.cnext[c]) S.cflags[c] &= ~CF_ISLAND;
+        for (;;) {
+            if (tid == 0) {
+                while (seed >= 0 && (bflag & (1u << seed))) --seed;
+                sh.isl_go = seed >= 0;
+                if (seed >= 0) {
+                    is.nb = 0; is.nc = 0;
+                    int* stack = sh.stack;
+                    int sc = 0;
+                    stack[sc++] = seed; bflag |= 1u << seed;
+                    while (sc > 0) {
+                        int b = stack[--sc];
+                        island_add_body(is, b);
+                        if (!is_dyn(b)) continue;
+                        for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
+                            int bA = L.fix_body[S.cfa[c]], bB = L.fix_body[S.cfb[c]];
+                            if (bA != b && bB != b) continue;
+                            if (S.cflags[c] & CF_ISLAND) continue;
+                            if ((S.cflags[c] & CF_ENABLED) == 0 || (S.cflags[c] & CF_TOUCHING) == 0) continue;
+                            is.contacts[is.nc++] = c;
+                            S.cflags[c] |= CF_ISLAND;
+                            int other = bA == b ? bB : bA;
+                            if (bflag & (1u << other)) continue;
+                            stack[sc++] = other; bflag |= 1u << other;
+                        }
+                    }
+                    island_pre(is, h, dtRatio, sh.u.sol.vcs, sh.u.sol.pcs);
                 }
             }
-            island_solve(is, h, dtRatio, sh.u.sol.vcs, sh.u.sol.pcs);
-            for (int i = 0; i < is.nb; ++i) if (!is_dyn(is.bodies[i])) bflag &= ~(1u << is.bodies[i]);
+            __syncthreads();
+            if (!sh.isl_go) break;
+            const int nc = is.nc;
+            if (nc > 0 && nc <= 64) solver_velocity_lanes(is, sh.u.sol.vcs, 180);
+            else if (nc > 64 && tid == 0) for (int it = 0; it < 180; ++it) solver_velocity(is, sh.u.sol.vcs);
+            __syncthreads();
+            if (tid == 0) {
+                island_post(is, h, sh.u.sol.vcs, sh.u.sol.pcs);
+                for (int i = 0; i < is.nb; ++i) if (!is_dyn(is.bodies[i])) bflag &= ~(1u << is.bodies[i]);
+                --seed;
+            }
         }
-        for (int b = ND - 1; b >= 0; --b) if (bflag & (1u << b)) sync_fixtures(b);
+        if (tid == 0) for (int b = ND - 1; b >= 0; --b) if (bflag & (1u << b)) sync_fixtures(b);
+        __syncthreads();
     }
 
     // ---------------------------------------------------------------- TOI
     __device__ __forceinline__ SweepV sweep(int b, const float* salpha0) const {
         SweepV s;
-        if (b < ND) { s.lcx = T.lcx[b]; s.lcy = T.lcy[b]; s.c0x = S.c0x[b]; s.c0y = S.c0y[b]; s.cx = S.cx[b]; s.cy = S.cy[b]; s.a0 = S.a0[b]; s.a = S.a[b]; s.alpha0 = S.alpha0[b]; }
-        else { s.lcx = 0.0f; s.lcy = 0.0f; s.c0x = s.cx = T.wall_px[b - ND]; s.c0y = s.cy = T.wall_py[b - ND]; s.a0 = s.a = 0.0f; s.alpha0 = salpha0[b - ND]; }
+        if (b < ND) { s.lcx = L.lcx[b]; s.lcy = L.lcy[b]; s.c0x = S.c0x[b]; s.c0y = S.c0y[b]; s.cx = S.cx[b]; s.cy = S.cy[b]; s.a0 = S.a0[b]; s.a = S.a[b]; s.alpha0 = S.alpha0[b]; }
+        else { s.lcx = 0.0f; s.lcy = 0.0f; s.c0x = s.cx = L.wall_px[b - ND]; s.c0y = s.cy = L.wall_py[b - ND]; s.a0 = s.a = 0.0f; s.alpha0 = salpha0[b - ND]; }
         return s;
     }
     __device__ __forceinline__ static Xf sweep_xf(const SweepV& s, float beta) {
@@ -1245,9 +1412,8 @@ template <int ENV> struct World {
             if (is_dyn(b)) { is.pcx[i] = S.cx[b]; is.pcy[i] = S.cy[b]; is.pa[i] = S.a[b]; is.vvx[i] = S.vx[b]; is.vvy[i] = S.vy[b]; is.vw[i] = S.w[b]; }
             else { V2 c = center(b); is.pcx[i] = c.x; is.pcy[i] = c.y; is.pa[i] = 0.0f; is.vvx[i] = 0.0f; is.vvy[i] = 0.0f; is.vw[i] = 0.0f; }
         }
-        MRP_TRACE(15, is.nc);
         solver_init(is, vcs, pcs, false, 1.0f);
-        for (int i = 0; i < 20; ++i) if (solver_position(is, pcs, true, toiA, toiB)) break;
+        for (int i = 0; i < 20; ++i) if (solver_position(is, vcs, pcs, true, toiA, toiB)) break;
         {
             int ba = is.bodies[toiA], bb = is.bodies[toiB];
             if (is_dyn(ba)) { S.c0x[ba] = is.pcx[toiA]; S.c0y[ba] = is.pcy[toiA]; S.a0[ba] = is.pa[toiA]; }
@@ -1278,7 +1444,7 @@ template <int ENV> struct World {
             if (S.ctoiCount[c] > MAX_SUBSTEPS) continue;
             if (S.cflags[c] & CF_TOI) { sh.plan[np] = -2; sh.pslot[np++] = c; continue; }
             int fa = S.cfa[c], fb = S.cfb[c];
-            int bA = T.fix_body[fa], bB = T.fix_body[fb];
+            int bA = L.fix_body[fa], bB = L.fix_body[fb];
             bool collideA = !is_dyn(bA), collideB = !is_dyn(bB);   // no bullets in these envs
             if (!collideA && !collideB) continue;
             SweepV sA = sweep(bA, salpha0), sB = sweep(bB, salpha0);
@@ -1313,7 +1479,7 @@ template <int ENV> struct World {
         if (minC == NULLN || 1.0f - 10.0f * FLT_EPS < minAlpha) { sh.toi_done = 1; return; }
         ++S.toiEvents;
         int fa = S.cfa[minC], fb = S.cfb[minC];
-        int bA = T.fix_body[fa], bB = T.fix_body[fb];
+        int bA = L.fix_body[fa], bB = L.fix_body[fb];
         SweepV back1 = sweep(bA, salpha0), back2 = sweep(bB, salpha0);
         body_advance(bA, minAlpha, salpha0);
         body_advance(bB, minAlpha, salpha0);
@@ -1339,7 +1505,7 @@ template <int ENV> struct World {
             int body = pair[k];
             if (!is_dyn(body)) continue;
             for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
-                int cA = T.fix_body[S.cfa[c]], cB = T.fix_body[S.cfb[c]];
+                int cA = L.fix_body[S.cfa[c]], cB = L.fix_body[S.cfb[c]];
                 if (cA != body && cB != body) continue;
                 if (is.nb == 2 * MAX_TOI_CONTACTS) break;
                 if (is.nc == MAX_TOI_CONTACTS) break;
@@ -1367,7 +1533,7 @@ template <int ENV> struct World {
             if (!is_dyn(body)) continue;
             sync_fixtures(body);
             for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
-                int cA = T.fix_body[S.cfa[c]], cB = T.fix_body[S.cfb[c]];
+                int cA = L.fix_body[S.cfa[c]], cB = L.fix_body[S.cfb[c]];
                 if (cA == body || cB == body) S.cflags[c] &= ~(CF_TOI | CF_ISLAND);
             }
         }
@@ -1387,8 +1553,8 @@ template <int ENV> struct World {
             for (int i = tid; i < tn; i += 64) {
                 int c = sh.tcand[i];
                 int fa = S.cfa[c], fb = S.cfb[c];
-                DProxy pA = {T.shape[fa].v, T.shape[fa].count, T.shape[fa].radius};
-                DProxy pB = {T.shape[fb].v, T.shape[fb].count, T.shape[fb].radius};
+                DProxy pA = {L.shape[fa].v, L.shape[fa].count, L.shape[fa].radius};
+                DProxy pB = {L.shape[fb].v, L.shape[fb].count, L.shape[fb].radius};
                 sh.u.toi.tout[i] = time_of_impact(pA, pB, sh.u.toi.tsA[i], sh.u.toi.tsB[i]);
             }
             __syncthreads();
@@ -1412,8 +1578,7 @@ template <int ENV> struct World {
         float dtRatio = S.inv_dt0 * dt;
         collide_coop();
         MRP_STAMP(3);
-        if (tid == 0) solve_serial(dt, dtRatio);
-        __syncthreads();
+        solve_coop(dt, dtRatio);
         MRP_STAMP(4);
         find_new_contacts_coop();
         MRP_STAMP(5);
