@@ -176,7 +176,8 @@ template <int ENV> struct Shared {
     uint32_t moved;
     int prox[LS::TN];
     // TOI scan bookkeeping
-    int tn, np, toi_done, toi_fnc;
+    int tn, np, toi_done, toi_fnc, toi_solve;
+    float toi_dt;
     int tcand[C];
     int plan[C];          // per list position: -2 cached, >= 0 candidate index
     int pslot[C];
@@ -1406,7 +1407,8 @@ template <int ENV> struct World {
     }
 
     // b2Island::SolveTOI
-    __device__ __forceinline__ void island_solve_toi(Isl& is, float dt, int toiA, int toiB, VC* vcs, PC* pcs, const float* salpha0) {
+    // b2Island::SolveTOI, first part (thread 0): position pre-solve and velocity constraints
+    __device__ __forceinline__ void island_toi_pre(Isl& is, int toiA, int toiB, VC* vcs, PC* pcs) {
         for (int i = 0; i < is.nb; ++i) {
             int b = is.bodies[i];
             if (is_dyn(b)) { is.pcx[i] = S.cx[b]; is.pcy[i] = S.cy[b]; is.pa[i] = S.a[b]; is.vvx[i] = S.vx[b]; is.vvy[i] = S.vy[b]; is.vw[i] = S.w[b]; }
@@ -1420,7 +1422,9 @@ template <int ENV> struct World {
             if (is_dyn(bb)) { S.c0x[bb] = is.pcx[toiB]; S.c0y[bb] = is.pcy[toiB]; S.a0[bb] = is.pa[toiB]; }
         }
         solver_init_velocity(is, vcs, pcs);
-        for (int i = 0; i < 180; ++i) solver_velocity(is, vcs);
+        // the 180 velocity sweeps run on the whole wave next (solve_toi_coop), then island_toi_post
+    }
+    __device__ __forceinline__ void island_toi_post(Isl& is, float dt) {
         integrate_positions(is, dt);
         for (int i = 0; i < is.nb; ++i) {
             int b = is.bodies[i];
@@ -1527,7 +1531,14 @@ template <int ENV> struct World {
                 island_add_body(is, other);
             }
         }
-        island_solve_toi(is, (1.0f - minAlpha) * dt, is.index[bA], is.index[bB], sh.u.sol.vcs, sh.u.sol.pcs, salpha0);
+        island_toi_pre(is, is.index[bA], is.index[bB], sh.u.sol.vcs, sh.u.sol.pcs);
+        sh.toi_dt = (1.0f - minAlpha) * dt;
+        sh.toi_solve = 1;   // velocity sweeps next (whole wave), then toi_event_post
+    }
+    // the rest of one TOI event after the island's velocity sweeps (thread 0)
+    __device__ __forceinline__ void toi_event_post() {
+        Isl& is = sh.isl;
+        island_toi_post(is, sh.toi_dt);
         for (int i = 0; i < is.nb; ++i) {
             int body = is.bodies[i];
             if (!is_dyn(body)) continue;
@@ -1558,8 +1569,16 @@ template <int ENV> struct World {
                 sh.u.toi.tout[i] = time_of_impact(pA, pB, sh.u.toi.tsA[i], sh.u.toi.tsB[i]);
             }
             __syncthreads();
-            if (tid == 0) toi_event(dt);
+            if (tid == 0) { sh.toi_solve = 0; toi_event(dt); }
             __syncthreads();
+            if (sh.toi_solve) {
+                const int nc = sh.isl.nc;
+                if (nc <= 64) solver_velocity_lanes(sh.isl, sh.u.sol.vcs, 180);
+                else if (tid == 0) for (int i = 0; i < 180; ++i) solver_velocity(sh.isl, sh.u.sol.vcs);
+                __syncthreads();
+                if (tid == 0) toi_event_post();
+                __syncthreads();
+            }
             if (sh.toi_done) break;
             if (sh.toi_fnc) find_new_contacts_coop();
         }
