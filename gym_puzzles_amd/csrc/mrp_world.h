@@ -914,9 +914,11 @@ template <int ENV> struct World {
     // ---------------------------------------------------------------- lane-distributed velocity sweeps
     // b2ContactSolver::SolveVelocityConstraints x `iters` with the island's constraint data held
     // in VGPRs across the wave: contact i's constants and impulses in lane i, island body k's
-    // velocity in lane k.  The Gauss-Seidel order is unchanged (one contact after another); each
-    // contact reads its operands with v_readlane and writes results back with a lane select, so the
-    // iters x nc contact updates never wait on LDS.  Float operations and their order are those
+    // velocity in lane k.  The Gauss-Seidel order is unchanged (one contact after another): for
+    // contact i every lane reads the two bodies' velocities with v_readlane and evaluates its own
+    // contact's update from its own registers, lane i's result is kept (impulses by a lane select,
+    // velocities by v_readlane + lane select into the body lanes), so the iters x nc contact
+    // updates never wait on LDS.  Float operations and their order are those
     // of solver_velocity, so the result is bitwise identical.  Every thread of the wave calls it;
     // needs is.nc <= 64.
     __device__ __forceinline__ static float rdl(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
@@ -925,7 +927,7 @@ template <int ENV> struct World {
     __device__ __forceinline__ float wrl(float old, float x, int l) const { return tid == l ? x : old; }
     __device__ __forceinline__ void solver_velocity_lanes(Isl& is, VC* vcs, int iters) {
         const int nc = is.nc;
-        const VC& my = vcs[tid < nc ? tid : 0];
+        const VC& my = vcs[tid < nc ? tid : 0];   // lanes >= nc evaluate a copy of contact 0 and are never kept
         const float rAx0 = my.rAx[0], rAy0 = my.rAy[0], rBx0 = my.rBx[0], rBy0 = my.rBy[0];
         const float rAx1 = my.rAx[1], rAy1 = my.rAy[1], rBx1 = my.rBx[1], rBy1 = my.rBy[1];
         const float nmass0 = my.nmass[0], nmass1 = my.nmass[1], tmass0 = my.tmass[0], tmass1 = my.tmass[1];
@@ -939,22 +941,24 @@ template <int ENV> struct World {
         float bvx = is.vvx[bk], bvy = is.vvy[bk], bw = is.vw[bk];
         for (int it = 0; it < iters; ++it) {
             for (int i = 0; i < nc; ++i) {
+                // every lane evaluates ITS contact's update from contact i's body velocities;
+                // only lane i's result is kept (the Gauss-Seidel order is contact by contact)
                 const int ia = rdli(cia, i), ib = rdli(cib, i), pcount = rdli(cpc, i);
-                const float mA = rdl(cmA, i), iA = rdl(ciA, i), mB = rdl(cmB, i), iB = rdl(ciB, i);
+                const bool mine = tid == i;
                 V2 vA = v2(rdl(bvx, ia), rdl(bvy, ia)); float wA = rdl(bw, ia);
                 V2 vB = v2(rdl(bvx, ib), rdl(bvy, ib)); float wB = rdl(bw, ib);
-                V2 normal = v2(rdl(cnx, i), rdl(cny, i)), tangent = vcross_vs(normal, 1.0f);
-                const float friction = rdl(cfr, i);
+                const float mA = cmA, iA = ciA, mB = cmB, iB = ciB;
+                V2 normal = v2(cnx, cny), tangent = vcross_vs(normal, 1.0f);
+                const float friction = cfr;
                 {   // friction, point 0
-                    V2 rA = v2(rdl(rAx0, i), rdl(rAy0, i)), rB = v2(rdl(rBx0, i), rdl(rBy0, i));
+                    V2 rA = v2(rAx0, rAy0), rB = v2(rBx0, rBy0);
                     V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
                     float vt = vdot(dv, tangent) - 0.0f;
-                    float lambda = rdl(tmass0, i) * (-vt);
-                    float maxFriction = friction * rdl(ni0, i);
-                    float told = rdl(ti0, i);
-                    float newImpulse = fclamp(told + lambda, -maxFriction, maxFriction);
-                    lambda = newImpulse - told;
-                    ti0 = wrl(ti0, newImpulse, i);
+                    float lambda = tmass0 * (-vt);
+                    float maxFriction = friction * ni0;
+                    float newImpulse = fclamp(ti0 + lambda, -maxFriction, maxFriction);
+                    lambda = newImpulse - ti0;
+                    if (mine) ti0 = newImpulse;
                     V2 P = vmul(lambda, tangent);
                     vA = vsub(vA, vmul(mA, P));
                     wA -= iA * vcross(rA, P);
@@ -962,15 +966,14 @@ template <int ENV> struct World {
                     wB += iB * vcross(rB, P);
                 }
                 if (pcount == 2) {   // friction, point 1
-                    V2 rA = v2(rdl(rAx1, i), rdl(rAy1, i)), rB = v2(rdl(rBx1, i), rdl(rBy1, i));
+                    V2 rA = v2(rAx1, rAy1), rB = v2(rBx1, rBy1);
                     V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
                     float vt = vdot(dv, tangent) - 0.0f;
-                    float lambda = rdl(tmass1, i) * (-vt);
-                    float maxFriction = friction * rdl(ni1, i);
-                    float told = rdl(ti1, i);
-                    float newImpulse = fclamp(told + lambda, -maxFriction, maxFriction);
-                    lambda = newImpulse - told;
-                    ti1 = wrl(ti1, newImpulse, i);
+                    float lambda = tmass1 * (-vt);
+                    float maxFriction = friction * ni1;
+                    float newImpulse = fclamp(ti1 + lambda, -maxFriction, maxFriction);
+                    lambda = newImpulse - ti1;
+                    if (mine) ti1 = newImpulse;
                     V2 P = vmul(lambda, tangent);
                     vA = vsub(vA, vmul(mA, P));
                     wA -= iA * vcross(rA, P);
@@ -978,42 +981,39 @@ template <int ENV> struct World {
                     wB += iB * vcross(rB, P);
                 }
                 if (pcount == 1) {
-                    V2 rA = v2(rdl(rAx0, i), rdl(rAy0, i)), rB = v2(rdl(rBx0, i), rdl(rBy0, i));
+                    V2 rA = v2(rAx0, rAy0), rB = v2(rBx0, rBy0);
                     V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
                     float vn = vdot(dv, normal);
-                    float nold = rdl(ni0, i);
-                    float lambda = -rdl(nmass0, i) * (vn - rdl(vbias0, i));
-                    float newImpulse = fmax_(nold + lambda, 0.0f);
-                    lambda = newImpulse - nold;
-                    ni0 = wrl(ni0, newImpulse, i);
+                    float lambda = -nmass0 * (vn - vbias0);
+                    float newImpulse = fmax_(ni0 + lambda, 0.0f);
+                    lambda = newImpulse - ni0;
+                    if (mine) ni0 = newImpulse;
                     V2 P = vmul(lambda, normal);
                     vA = vsub(vA, vmul(mA, P));
                     wA -= iA * vcross(rA, P);
                     vB = vadd(vB, vmul(mB, P));
                     wB += iB * vcross(rB, P);
                 } else {
-                    V2 r1A = v2(rdl(rAx0, i), rdl(rAy0, i)), r1B = v2(rdl(rBx0, i), rdl(rBy0, i));
-                    V2 r2A = v2(rdl(rAx1, i), rdl(rAy1, i)), r2B = v2(rdl(rBx1, i), rdl(rBy1, i));
-                    const float K0 = rdl(k0, i), K1 = rdl(k1, i), K2 = rdl(k2, i), K3 = rdl(k3, i);
-                    const float M0 = rdl(nm0, i), M1 = rdl(nm1, i), M2 = rdl(nm2, i), M3 = rdl(nm3, i);
-                    V2 a = v2(rdl(ni0, i), rdl(ni1, i));
+                    V2 r1A = v2(rAx0, rAy0), r1B = v2(rBx0, rBy0);
+                    V2 r2A = v2(rAx1, rAy1), r2B = v2(rBx1, rBy1);
+                    V2 a = v2(ni0, ni1);
                     V2 dv1 = vsub(vsub(vadd(vB, vcross_sv(wB, r1B)), vA), vcross_sv(wA, r1A));
                     V2 dv2 = vsub(vsub(vadd(vB, vcross_sv(wB, r2B)), vA), vcross_sv(wA, r2A));
                     float vn1 = vdot(dv1, normal), vn2 = vdot(dv2, normal);
-                    V2 b = v2(vn1 - rdl(vbias0, i), vn2 - rdl(vbias1, i));
-                    b = vsub(b, v2(K0 * a.x + K2 * a.y, K1 * a.x + K3 * a.y));
+                    V2 b = v2(vn1 - vbias0, vn2 - vbias1);
+                    b = vsub(b, v2(k0 * a.x + k2 * a.y, k1 * a.x + k3 * a.y));
                     V2 x;
                     bool ok = false;
-                    x = vneg(v2(M0 * b.x + M2 * b.y, M1 * b.x + M3 * b.y));
+                    x = vneg(v2(nm0 * b.x + nm2 * b.y, nm1 * b.x + nm3 * b.y));
                     if (x.x >= 0.0f && x.y >= 0.0f) ok = true;
                     if (!ok) {
-                        x.x = -rdl(nmass0, i) * b.x; x.y = 0.0f;
-                        vn2 = K1 * x.x + b.y;
+                        x.x = -nmass0 * b.x; x.y = 0.0f;
+                        vn2 = k1 * x.x + b.y;
                         if (x.x >= 0.0f && vn2 >= 0.0f) ok = true;
                     }
                     if (!ok) {
-                        x.x = 0.0f; x.y = -rdl(nmass1, i) * b.y;
-                        vn1 = K2 * x.y + b.x;
+                        x.x = 0.0f; x.y = -nmass1 * b.y;
+                        vn1 = k2 * x.y + b.x;
                         if (x.y >= 0.0f && vn1 >= 0.0f) ok = true;
                     }
                     if (!ok) {
@@ -1027,11 +1027,14 @@ template <int ENV> struct World {
                         wA -= iA * (vcross(r1A, P1) + vcross(r2A, P2));
                         vB = vadd(vB, vmul(mB, vadd(P1, P2)));
                         wB += iB * (vcross(r1B, P1) + vcross(r2B, P2));
-                        ni0 = wrl(ni0, x.x, i); ni1 = wrl(ni1, x.y, i);
+                        if (mine) { ni0 = x.x; ni1 = x.y; }
                     }
                 }
-                bvx = wrl(bvx, vA.x, ia); bvy = wrl(bvy, vA.y, ia); bw = wrl(bw, wA, ia);
-                bvx = wrl(bvx, vB.x, ib); bvy = wrl(bvy, vB.y, ib); bw = wrl(bw, wB, ib);
+                // lane i's results go to the lanes of bodies A and B (A first, as the reference stores)
+                const float nAx = rdl(vA.x, i), nAy = rdl(vA.y, i), nwA = rdl(wA, i);
+                const float nBx = rdl(vB.x, i), nBy = rdl(vB.y, i), nwB = rdl(wB, i);
+                bvx = wrl(bvx, nAx, ia); bvy = wrl(bvy, nAy, ia); bw = wrl(bw, nwA, ia);
+                bvx = wrl(bvx, nBx, ib); bvy = wrl(bvy, nBy, ib); bw = wrl(bw, nwB, ib);
             }
         }
         if (tid < is.nb) { is.vvx[tid] = bvx; is.vvy[tid] = bvy; is.vw[tid] = bw; }
