@@ -35,17 +35,20 @@ typedef uint32_t __attribute__((__may_alias__)) word_t;
 
 template <int ENV>
 __device__ __forceinline__ void load_state(LaneState<ENV>& S, const uint32_t* __restrict__ g, int lane, int tid) {
-    word_t* w = reinterpret_cast<word_t*>(&S);
-    constexpr int NW = lane_words<ENV>();
-    const uint32_t* src = g + (size_t)lane * NW;
-    for (int i = tid; i < NW; i += BLOCK) w[i] = src[i];
+    static_assert(sizeof(LaneState<ENV>) % 16 == 0, "lane state moves in 16-B granules");
+    constexpr int NQ = (int)(sizeof(LaneState<ENV>) / 16);
+    typedef uint4 __attribute__((__may_alias__)) quad_t;
+    quad_t* w = reinterpret_cast<quad_t*>(&S);
+    const quad_t* src = reinterpret_cast<const quad_t*>(g + (size_t)lane * lane_words<ENV>());
+    for (int i = tid; i < NQ; i += BLOCK) w[i] = src[i];
 }
 template <int ENV>
 __device__ __forceinline__ void store_state(const LaneState<ENV>& S, uint32_t* __restrict__ g, int lane, int tid) {
-    const word_t* w = reinterpret_cast<const word_t*>(&S);
-    constexpr int NW = lane_words<ENV>();
-    uint32_t* dst = g + (size_t)lane * NW;
-    for (int i = tid; i < NW; i += BLOCK) dst[i] = w[i];
+    constexpr int NQ = (int)(sizeof(LaneState<ENV>) / 16);
+    typedef uint4 __attribute__((__may_alias__)) quad_t;
+    const quad_t* w = reinterpret_cast<const quad_t*>(&S);
+    quad_t* dst = reinterpret_cast<quad_t*>(g + (size_t)lane * lane_words<ENV>());
+    for (int i = tid; i < NQ; i += BLOCK) dst[i] = w[i];
 }
 
 // copy this env's hot tables from __constant__ memory into the lane's LDS (before the

@@ -68,7 +68,7 @@ constexpr float FLT_MAXV = 3.40282346638528859811704183484516925e+38f;
 constexpr int CF_ISLAND = 1, CF_TOUCHING = 2, CF_ENABLED = 4, CF_TOI = 32;
 constexpr int MT_FACEA = 1, MT_FACEB = 2;
 
-template <int ENV> struct LaneState {
+template <int ENV> struct alignas(16) LaneState {   // 16-B granules: moved with dwordx4 per thread
     using D = Dims<ENV>;
     static constexpr int ND = D::NA + D::NB;
     static constexpr int C = D::CMAX;
