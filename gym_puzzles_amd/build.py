@@ -16,8 +16,11 @@ OUT = os.path.join(HERE, "libmrp.so")
 SOURCES = [os.path.join(CSRC, "mrp_kernels.hip"), os.path.join(CSRC, "mrp_tables.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("mrp_math.h", "mrp_config.h", "mrp_world.h", "mrp_env.h", "mrp_tables.h")] + [
     os.path.join(HERE, "..", "include", "mrp.h")]
+# -fno-slp-vectorize: the serial solver chains are latency-bound; packing pairs of f32 ops into
+# v_pk_* costs operand-shuffling moves on the dependency chain (measured +2-3 % env-steps/s off)
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
-         "-fno-gpu-flush-denormals-to-zero", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-strict-aliasing", "-fPIC", "-shared"]
+         "-fno-gpu-flush-denormals-to-zero", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-strict-aliasing",
+         "-fno-slp-vectorize", "-fPIC", "-shared"]
 
 
 def hipcc() -> str:
