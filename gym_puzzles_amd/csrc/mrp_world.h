@@ -114,8 +114,8 @@ struct TOIOut { int state; float t; };
 struct ClipV { V2 v; uint32_t id; };
 struct VC {
     float rAx[2], rAy[2], rBx[2], rBy[2], ni[2], ti[2], nmass[2], tmass[2], vbias[2];
-    float nx, ny, nm0, nm1, nm2, nm3, k0, k1, k2, k3;
-    float mA, mB, iA, iB, friction, restitution;
+    float nx, ny, nm0, nm1, nm3, k0, k1, k3;   // K and K^-1 are symmetric: k2 == k1, nm2 == nm1 (not stored)
+    float mA, mB, iA, iB, friction;
     int iaI, ibI, pointCount, slot;
 };
 struct PC {   // position constraint; body indices and mass data are read from the contact's VC
@@ -668,11 +668,11 @@ template <int ENV> struct World {
             int bA = L.fix_body[fa], bB = L.fix_body[fb];
             int pcount = S.mpc[c];
             VC& vc = vcs[i];
-            vc.friction = S.cfric[c]; vc.restitution = fmax_(L.fix_restitution[fa], L.fix_restitution[fb]);
+            vc.friction = S.cfric[c];
             vc.iaI = is.index[bA]; vc.ibI = is.index[bB];
             vc.mA = L.invMass[bA]; vc.mB = L.invMass[bB]; vc.iA = L.invI[bA]; vc.iB = L.invI[bB];
             vc.slot = c; vc.pointCount = pcount;
-            vc.k0 = vc.k1 = vc.k2 = vc.k3 = 0.0f; vc.nm0 = vc.nm1 = vc.nm2 = vc.nm3 = 0.0f;
+            vc.k0 = vc.k1 = vc.k3 = 0.0f; vc.nm0 = vc.nm1 = vc.nm3 = 0.0f;
             PC& pc = pcs[i];
             pc.lcAx = L.lcx[bA]; pc.lcAy = L.lcy[bA]; pc.lcBx = L.lcx[bB]; pc.lcBy = L.lcy[bB];
             pc.lnx = S.mlnx[c]; pc.lny = S.mlny[c]; pc.lpx0 = S.mlpx[c]; pc.lpy0 = S.mlpy[c];
@@ -690,6 +690,7 @@ template <int ENV> struct World {
         for (int i = 0; i < is.nc; ++i) {
             VC& vc = vcs[i]; PC& pc = pcs[i];
             int c = vc.slot;
+            const float restitution = fmax_(L.fix_restitution[S.cfa[c]], L.fix_restitution[S.cfb[c]]);
             int ia = vc.iaI, ib = vc.ibI;
             float mA = vc.mA, mB = vc.mB, iA = vc.iA, iB = vc.iB;
             V2 cA = v2(is.pcx[ia], is.pcy[ia]); float aA = is.pa[ia];
@@ -737,7 +738,7 @@ template <int ENV> struct World {
                 vc.vbias[j] = 0.0f;
                 V2 dvr = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
                 float vRel = vdot(normal, dvr);
-                if (vRel < -VELOCITY_THRESHOLD) vc.vbias[j] = -vc.restitution * vRel;
+                if (vRel < -VELOCITY_THRESHOLD) vc.vbias[j] = -restitution * vRel;
             }
             if (vc.pointCount == 2) {
                 float rn1A = vcross(v2(vc.rAx[0], vc.rAy[0]), normal), rn1B = vcross(v2(vc.rBx[0], vc.rBy[0]), normal);
@@ -747,11 +748,11 @@ template <int ENV> struct World {
                 float k12 = mA + mB + iA * rn1A * rn2A + iB * rn1B * rn2B;
                 const float k_maxConditionNumber = 1000.0f;
                 if (k11 * k11 < k_maxConditionNumber * (k11 * k22 - k12 * k12)) {
-                    vc.k0 = k11; vc.k1 = k12; vc.k2 = k12; vc.k3 = k22;
-                    float a = vc.k0, b = vc.k2, cc = vc.k1, d = vc.k3;
+                    vc.k0 = k11; vc.k1 = k12; vc.k3 = k22;   // k2 = k12 too
+                    float a = vc.k0, b = vc.k1, cc = vc.k1, d = vc.k3;
                     float det = a * d - b * cc;
                     if (det != 0.0f) det = 1.0f / det;
-                    vc.nm0 = det * d; vc.nm2 = -det * b; vc.nm1 = -det * cc; vc.nm3 = det * a;
+                    vc.nm0 = det * d; vc.nm1 = -det * cc; vc.nm3 = det * a;   // nm2 = -det * b == nm1
                 } else {
                     vc.pointCount = 1;
                 }
@@ -821,10 +822,10 @@ template <int ENV> struct World {
                 V2 dv2 = vsub(vsub(vadd(vB, vcross_sv(wB, r2B)), vA), vcross_sv(wA, r2A));
                 float vn1 = vdot(dv1, normal), vn2 = vdot(dv2, normal);
                 V2 b = v2(vn1 - vc.vbias[0], vn2 - vc.vbias[1]);
-                b = vsub(b, v2(vc.k0 * a.x + vc.k2 * a.y, vc.k1 * a.x + vc.k3 * a.y));
+                b = vsub(b, v2(vc.k0 * a.x + vc.k1 * a.y, vc.k1 * a.x + vc.k3 * a.y));
                 V2 x;
                 bool ok = false;
-                x = vneg(v2(vc.nm0 * b.x + vc.nm2 * b.y, vc.nm1 * b.x + vc.nm3 * b.y));
+                x = vneg(v2(vc.nm0 * b.x + vc.nm1 * b.y, vc.nm1 * b.x + vc.nm3 * b.y));
                 if (x.x >= 0.0f && x.y >= 0.0f) ok = true;
                 if (!ok) {
                     x.x = -vc.nmass[0] * b.x; x.y = 0.0f;
@@ -833,7 +834,7 @@ template <int ENV> struct World {
                 }
                 if (!ok) {
                     x.x = 0.0f; x.y = -vc.nmass[1] * b.y;
-                    vn1 = vc.k2 * x.y + b.x;
+                    vn1 = vc.k1 * x.y + b.x;
                     if (x.y >= 0.0f && vn1 >= 0.0f) ok = true;
                 }
                 if (!ok) {
@@ -932,8 +933,8 @@ template <int ENV> struct World {
         const float rAx1 = my.rAx[1], rAy1 = my.rAy[1], rBx1 = my.rBx[1], rBy1 = my.rBy[1];
         const float nmass0 = my.nmass[0], nmass1 = my.nmass[1], tmass0 = my.tmass[0], tmass1 = my.tmass[1];
         const float vbias0 = my.vbias[0], vbias1 = my.vbias[1];
-        const float cnx = my.nx, cny = my.ny, k0 = my.k0, k1 = my.k1, k2 = my.k2, k3 = my.k3;
-        const float nm0 = my.nm0, nm1 = my.nm1, nm2 = my.nm2, nm3 = my.nm3;
+        const float cnx = my.nx, cny = my.ny, k0 = my.k0, k1 = my.k1, k2 = my.k1, k3 = my.k3;
+        const float nm0 = my.nm0, nm1 = my.nm1, nm2 = my.nm1, nm3 = my.nm3;
         const float cmA = my.mA, cmB = my.mB, ciA = my.iA, ciB = my.iB, cfr = my.friction;
         const int cia = my.iaI, cib = my.ibI, cpc = my.pointCount;
         float ni0 = my.ni[0], ni1 = my.ni[1], ti0 = my.ti[0], ti1 = my.ti[1];
