@@ -5,6 +5,8 @@ gym_puzzles env interface.  See DESIGN.md.
     envs.MultiRobotPuzzle  gym-style single env classes (same names as gym_puzzles.envs)
     envs.make(id)          gym.make equivalent (adds gym 0.21's TimeLimit)
     MultiRobotPuzzleVecEnv SB3-style vectorised env with on-device auto-reset
+    MultiRobotPuzzleVecNormalize / DeviceVecNormalize
+                           SB3 VecNormalize + Monitor statistics on the device
 """
 from ._native import ENV_IDS, Batch, MrpError, env_dims  # noqa: F401
 
@@ -15,7 +17,7 @@ def __getattr__(name):
                 "MultiRobotPuzzleHeavy2ThreeBlock", "make"):
         from . import envs
         return getattr(envs, name)
-    if name == "MultiRobotPuzzleVecEnv":
-        from .vec_env import MultiRobotPuzzleVecEnv
-        return MultiRobotPuzzleVecEnv
+    if name in ("MultiRobotPuzzleVecEnv", "MultiRobotPuzzleVecNormalize", "DeviceVecNormalize"):
+        from . import vec_env
+        return getattr(vec_env, name)
     raise AttributeError(name)

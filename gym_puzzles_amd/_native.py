@@ -32,7 +32,8 @@ EXPORTED = (
     "mrp_reset", "mrp_reset_device", "mrp_step", "mrp_step_device", "mrp_set_auto_reset",
     "mrp_get_bodies", "mrp_get_flags", "mrp_counters", "mrp_state_words", "mrp_get_state", "mrp_set_state",
     "mrp_set_time_limit", "mrp_selftest_sincos", "mrp_debug_stamps", "mrp_debug_stamps_ext",
-    "mrp_debug_trace",
+    "mrp_debug_trace", "mrp_norm_create", "mrp_norm_destroy", "mrp_norm_last_error", "mrp_norm_set_stream",
+    "mrp_norm_set_training", "mrp_norm_reset_device", "mrp_norm_step_device", "mrp_norm_get_stats", "mrp_norm_set_stats",
 )
 
 _lib = None
@@ -80,6 +81,17 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.mrp_set_time_limit.argtypes = [P, i]
     L.mrp_selftest_sincos.argtypes = [i, P, P, P, i]
     L.mrp_debug_stamps.argtypes = [i, P]
+    L.mrp_norm_create.argtypes = [i, i, i, d, d, d, d, ctypes.POINTER(P)]
+    L.mrp_norm_destroy.argtypes = [P]
+    L.mrp_norm_destroy.restype = None
+    L.mrp_norm_last_error.argtypes = [P]
+    L.mrp_norm_last_error.restype = ctypes.c_char_p
+    L.mrp_norm_set_stream.argtypes = [P, P]
+    L.mrp_norm_set_training.argtypes = [P, i]
+    L.mrp_norm_reset_device.argtypes = [P, P, P]
+    L.mrp_norm_step_device.argtypes = [P] * 10
+    L.mrp_norm_get_stats.argtypes = [P, P]
+    L.mrp_norm_set_stats.argtypes = [P, P]
     for name, args in (("mrp_debug_stamps_ext", [i, P, P, P]), ("mrp_debug_trace", [i, P, i])):
         if hasattr(L, name):   # diagnostics: absent from older builds
             getattr(L, name).argtypes = args

@@ -13,7 +13,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmrp.so")
-SOURCES = [os.path.join(CSRC, "mrp_kernels.hip"), os.path.join(CSRC, "mrp_tables.cpp")]
+SOURCES = [os.path.join(CSRC, "mrp_kernels.hip"), os.path.join(CSRC, "mrp_tables.cpp"), os.path.join(CSRC, "mrp_norm.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("mrp_math.h", "mrp_config.h", "mrp_world.h", "mrp_env.h", "mrp_tables.h")] + [
     os.path.join(HERE, "..", "include", "mrp.h")]
 # -fno-slp-vectorize: the serial solver chains are latency-bound; packing pairs of f32 ops into

@@ -374,7 +374,7 @@ int mrp_create(int env_id, int n_lanes, int device, uint64_t seed, uint64_t lane
 
 int mrp_set_stream(mrp_ctx* ctx, void* hip_stream) {
     if (!ctx) return MRP_E_ARG;
-    ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+    ctx->stream = (hipStream_t)hip_stream;   // NULL: the HIP null stream (torch's default stream)
     return MRP_OK;
 }
 

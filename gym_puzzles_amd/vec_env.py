@@ -123,3 +123,138 @@ class MultiRobotPuzzleVecEnv:
     @property
     def batch(self) -> Batch:
         return self._b
+
+
+class DeviceVecNormalize:
+    """stable-baselines3 ``VecNormalize`` + ``Monitor`` statistics kept on the GPU (libmrp's
+    ``mrp_norm_*``).  The reference wraps every env in ``Monitor`` and the vector
+    env in ``VecNormalize`` with default arguments (``train/train.py:68,80-82``).  All arrays are
+    torch CUDA tensors on ``device``; calls are asynchronous on the current torch stream."""
+
+    def __init__(self, n_lanes: int, obs_dim: int, device: int = 0, clip_obs: float = 10.0, clip_reward: float = 10.0,
+                 gamma: float = 0.99, epsilon: float = 1e-8):
+        import ctypes
+
+        from ._native import MrpError, load
+        self._L, self._err = load(), MrpError
+        self.n_lanes, self.obs_dim, self.device = n_lanes, obs_dim, device
+        h = ctypes.c_void_p()
+        rc = self._L.mrp_norm_create(n_lanes, obs_dim, device, clip_obs, clip_reward, gamma, epsilon, ctypes.byref(h))
+        if rc != 0:
+            raise MrpError(f"mrp_norm_create failed ({rc}): {self._L.mrp_norm_last_error(None).decode()}")
+        self._h = h
+        self._training = True
+
+    def _check(self, rc):
+        if rc != 0:
+            raise self._err(self._L.mrp_norm_last_error(self._h).decode())
+
+    def _sync_stream(self):
+        import torch
+        self._check(self._L.mrp_norm_set_stream(self._h, torch.cuda.current_stream(self.device).cuda_stream))
+
+    @property
+    def training(self) -> bool:
+        return self._training
+
+    @training.setter
+    def training(self, value: bool):
+        self._training = bool(value)
+        self._check(self._L.mrp_norm_set_training(self._h, int(self._training)))
+
+    def reset(self, obs, obs_out):
+        self._sync_stream()
+        self._check(self._L.mrp_norm_reset_device(self._h, obs.data_ptr(), obs_out.data_ptr()))
+
+    def step(self, obs, reward, done, obs_out, reward_out, term_obs=None, term_out=None, ep_return=None, ep_len=None):
+        ptr = (lambda t: None if t is None else t.data_ptr())
+        self._sync_stream()
+        self._check(self._L.mrp_norm_step_device(self._h, ptr(obs), ptr(reward), ptr(done), ptr(term_obs), ptr(obs_out),
+                                                  ptr(reward_out), ptr(term_out), ptr(ep_return), ptr(ep_len)))
+
+    def get_stats(self) -> dict:
+        st = np.zeros(2 * self.obs_dim + 4, np.float64)
+        self._check(self._L.mrp_norm_get_stats(self._h, st.ctypes.data))
+        D = self.obs_dim
+        return {"obs_mean": st[:D], "obs_var": st[D:2 * D], "obs_count": st[2 * D], "ret_mean": st[2 * D + 1],
+                "ret_var": st[2 * D + 2], "ret_count": st[2 * D + 3]}
+
+    def set_stats(self, stats: dict) -> None:
+        st = np.concatenate([np.asarray(stats["obs_mean"], np.float64), np.asarray(stats["obs_var"], np.float64),
+                             [stats["obs_count"], stats["ret_mean"], stats["ret_var"], stats["ret_count"]]])
+        self._check(self._L.mrp_norm_set_stats(self._h, np.ascontiguousarray(st).ctypes.data))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.mrp_norm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MultiRobotPuzzleVecNormalize:
+    """``VecNormalize(MultiRobotPuzzleVecEnv)`` with ``Monitor`` episode records, computed on the
+    device.  Same VecEnv surface as SB3's wrapper: ``reset()`` / ``step(actions)`` return host
+    numpy arrays (normalised obs and reward), ``infos[i]`` carry ``terminal_observation``
+    (normalised), ``TimeLimit.truncated`` and Monitor's ``episode`` = {"r", "l"} for finished
+    lanes; ``get_original_obs()`` / ``get_original_reward()`` give the raw values."""
+
+    def __init__(self, venv: MultiRobotPuzzleVecEnv, training: bool = True, clip_obs: float = 10.0,
+                 clip_reward: float = 10.0, gamma: float = 0.99, epsilon: float = 1e-8):
+        import torch
+        self.venv = venv
+        self.num_envs, self.observation_space, self.action_space = venv.num_envs, venv.observation_space, venv.action_space
+        N, O = venv.num_envs, venv.observation_space.shape[0]
+        dev = torch.device("cuda", venv.device)
+        self.norm = DeviceVecNormalize(N, O, venv.device, clip_obs, clip_reward, gamma, epsilon)
+        self.norm.training = training
+        z = lambda *s, dt=torch.float32: torch.zeros(s, dtype=dt, device=dev)  # noqa: E731
+        self._act, self._obs, self._rew = z(N, venv.action_space.shape[0]), z(N, O), z(N)
+        self._done, self._trunc, self._term = z(N, dt=torch.uint8), z(N, dt=torch.uint8), z(N, O)
+        self._nobs, self._nrew, self._nterm = z(N, O), z(N), z(N, O)
+        self._epr, self._epl = z(N, dt=torch.float64), z(N, dt=torch.int32)
+
+    @property
+    def training(self):
+        return self.norm.training
+
+    @training.setter
+    def training(self, v):
+        self.norm.training = v
+
+    def reset(self):
+        import torch
+        self._obs.copy_(torch.from_numpy(self.venv.reset()))
+        self.norm.reset(self._obs, self._nobs)
+        return self._nobs.cpu().numpy()
+
+    def step(self, actions):
+        import torch
+        self._act.copy_(torch.as_tensor(np.asarray(actions, np.float32).reshape(self.num_envs, -1)))
+        self.venv.step_torch(self._act, self._obs, self._rew, self._done, self._trunc, self._term)
+        self.norm.step(self._obs, self._rew, self._done, self._nobs, self._nrew, self._term, self._nterm, self._epr, self._epl)
+        obs, rew = self._nobs.cpu().numpy(), self._nrew.cpu().numpy()
+        done, trunc = self._done.cpu().numpy().astype(bool), self._trunc.cpu().numpy().astype(bool)
+        infos = [{} for _ in range(self.num_envs)]
+        idx = np.nonzero(done)[0]
+        if idx.size:
+            term, epr, epl = self._nterm.cpu().numpy(), self._epr.cpu().numpy(), self._epl.cpu().numpy()
+            for i in idx:
+                infos[i]["terminal_observation"] = term[i].copy()
+                infos[i]["TimeLimit.truncated"] = bool(trunc[i])
+                infos[i]["episode"] = {"r": round(float(epr[i]), 6), "l": int(epl[i])}
+        return obs, rew, done, infos
+
+    def get_original_obs(self):
+        return self._obs.cpu().numpy()
+
+    def get_original_reward(self):
+        return self._rew.cpu().numpy()
+
+    def close(self):
+        self.norm.close()
+        self.venv.close()

@@ -60,7 +60,8 @@ const char* mrp_last_error(const mrp_ctx* ctx);
 int mrp_n_lanes(const mrp_ctx* ctx);
 int mrp_env_id(const mrp_ctx* ctx);
 
-/* Use this hipStream_t (NULL = the context's own stream) for all subsequent work. */
+/* Use this hipStream_t for all subsequent work; NULL selects the HIP null stream (torch's default
+ * stream, cuda_stream == 0).  A new context runs on its own non-blocking stream until this is called. */
 int mrp_set_stream(mrp_ctx* ctx, void* hip_stream);
 int mrp_synchronize(mrp_ctx* ctx);
 
@@ -128,6 +129,37 @@ int mrp_debug_stamps_ext(int device, uint64_t* pmax16, uint64_t* stepmax256, uin
 /* Diagnostic builds only: the last step's per-lane trace, n_lanes x 16 words (phase cycles 0-10,
  * total, island contacts, TOI events, position iterations, velocity-solver contact units). */
 int mrp_debug_trace(int device, uint32_t* out, int n_lanes);
+
+/* ------------------------------------------------------------------------------------------
+ * On-device VecNormalize + Monitor statistics.  Replaces the host-side
+ * stable-baselines3 wrappers the reference trains with: Monitor(env) per env
+ * (train/train.py:68) and VecNormalize(DummyVecEnv(...)) with default arguments
+ * (train/train.py:80-82; loaded back by train/test.py:66).  The statistics live on the device;
+ * inputs and outputs are device arrays of a step's outputs ([n_lanes][obs_dim] float32 obs,
+ * [n_lanes] float32 reward, uint8 done).  Asynchronous on the context's stream.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct mrp_norm mrp_norm;
+
+/* VecNormalize(clip_obs, clip_reward, gamma, epsilon); RunningMeanStd(epsilon=1e-4) for obs and returns */
+int mrp_norm_create(int n_lanes, int obs_dim, int device, double clip_obs, double clip_reward, double gamma, double epsilon,
+                    mrp_norm** out);
+void mrp_norm_destroy(mrp_norm* n);
+const char* mrp_norm_last_error(const mrp_norm* n);
+int mrp_norm_set_stream(mrp_norm* n, void* hip_stream);   /* as mrp_set_stream: NULL = the HIP null stream */
+/* VecNormalize.training: statistics update on (1) or frozen (0, evaluation) */
+int mrp_norm_set_training(mrp_norm* n, int training);
+/* VecNormalize.reset: update obs statistics, normalise obs, zero the discounted returns and
+ * the Monitor accumulators */
+int mrp_norm_reset_device(mrp_norm* n, const float* d_obs, float* d_obs_out);
+/* VecNormalize.step_wait + Monitor.step: normalised obs / reward (and terminal obs of done
+ * lanes, optional), returns[done] = 0; for done lanes the finished episode's return (float64
+ * sum of raw rewards) and length (Monitor's info["episode"] r / l; optional outputs) */
+int mrp_norm_step_device(mrp_norm* n, const float* d_obs, const float* d_reward, const uint8_t* d_done, const float* d_term_obs,
+                         float* d_obs_out, float* d_reward_out, float* d_term_out, double* d_ep_return, int32_t* d_ep_len);
+/* statistics as float64[2*obs_dim + 4]: obs mean[obs_dim], obs var[obs_dim], obs count,
+ * return mean, return var, return count (VecNormalize save/load) */
+int mrp_norm_get_stats(mrp_norm* n, double* out);
+int mrp_norm_set_stats(mrp_norm* n, const double* in);
 
 #ifdef __cplusplus
 }

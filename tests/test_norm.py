@@ -1,0 +1,119 @@
+"""On-device VecNormalize + Monitor statistics (mrp_norm.hip) against the numpy
+restatement of stable-baselines3's algorithm (oracle/vecnorm_ref.py; SB3 is not installed, so
+parity with SB3 itself is unpinned).
+
+Tolerances: batch moments are float64 on both sides but summed in a different order (a
+256-thread tree on the device, numpy's pairwise sum here), so statistics agree to rtol 1e-12 and
+normalised float32 outputs to 2 ulp-scale (rtol 1e-6, atol 1e-6).  Monitor episode returns are
+sequential float64 sums of the same float32 rewards in the same order: bit-exact.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+
+def test_running_mean_std_merge_is_batch_invariant():
+    from oracle.vecnorm_ref import RunningMeanStd
+    rs = np.random.RandomState(0)
+    x = rs.normal(3.0, 2.0, size=(600, 5))
+    a, b = RunningMeanStd((5,)), RunningMeanStd((5,))
+    a.update(x)
+    for k in range(0, 600, 150):
+        b.update(x[k:k + 150])
+    np.testing.assert_allclose(a.mean, b.mean, rtol=1e-12)
+    np.testing.assert_allclose(a.var, b.var, rtol=1e-9)
+    assert a.count == pytest.approx(600 + 1e-4) and b.count == pytest.approx(600 + 1e-4)
+    # the epsilon-count prior barely moves the batch moments
+    np.testing.assert_allclose(a.mean, x.mean(0), rtol=1e-6)
+    np.testing.assert_allclose(a.var, x.var(0), rtol=1e-5)
+
+
+def test_vecnormalize_restatement_semantics():
+    from oracle.vecnorm_ref import VecNormalizeRef
+    n = VecNormalizeRef(4, 2, clip_obs=1.0)
+    o = n.reset(np.array([[0, 0], [1, 1], [2, 2], [3, 3]], np.float32))
+    assert o.dtype == np.float32 and np.all(np.abs(o) <= 1.0)
+    r = np.array([1, 2, 3, 4], np.float32)
+    _, rn, _, er, el = n.step(np.zeros((4, 2), np.float32), r, np.array([0, 1, 0, 0], np.uint8))
+    np.testing.assert_allclose(n.returns, [1, 0, 3, 4])          # returns[done] = 0 after the update
+    assert er[1] == 2.0 and el[1] == 1 and n.ep_len[1] == 0 and n.ep_len[0] == 1
+    assert np.all(np.abs(rn) <= 10.0)
+    n.training = False
+    before = n.obs_rms.mean.copy()
+    n.step(np.ones((4, 2), np.float32), r, np.zeros(4, np.uint8))
+    np.testing.assert_array_equal(n.obs_rms.mean, before)      # frozen statistics in evaluation
+
+
+@pytest.mark.gpu
+def test_device_vecnormalize_matches_restatement(gpu_lib):
+    import torch
+
+    from gym_puzzles_amd import Batch, DeviceVecNormalize
+    from oracle.vecnorm_ref import VecNormalizeRef
+    lanes, steps = 1024, 120
+    dev = torch.device("cuda", 0)
+    b = Batch(0, lanes, seed=21)
+    b.set_auto_reset(True)
+    b.set_time_limit(40)                 # every lane finishes episodes inside the run
+    O = b.obs_dim
+    norm = DeviceVecNormalize(lanes, O, 0)
+    ref = VecNormalizeRef(lanes, O)
+    obs0 = torch.from_numpy(b.reset().copy()).to(dev)
+    nobs = torch.zeros_like(obs0)
+    norm.reset(obs0, nobs)
+    np.testing.assert_allclose(nobs.cpu().numpy(), ref.reset(obs0.cpu().numpy()), rtol=1e-6, atol=1e-6)
+    z = lambda *s, dt=torch.float32: torch.zeros(s, dtype=dt, device=dev)  # noqa: E731
+    obs, rew, done, trunc, term = z(lanes, O), z(lanes), z(lanes, dt=torch.uint8), z(lanes, dt=torch.uint8), z(lanes, O)
+    nrew, nterm, epr, epl = z(lanes), z(lanes, O), z(lanes, dt=torch.float64), z(lanes, dt=torch.int32)
+    s = torch.cuda.current_stream(dev)
+    b.set_stream(s.cuda_stream)
+    n_done = 0
+    for t in range(steps):
+        b.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), trunc.data_ptr(), 0, term.data_ptr())
+        norm.step(obs, rew, done, nobs, nrew, term, nterm, epr, epl)
+        ho, hr, hd, ht = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy(), term.cpu().numpy()
+        o, r, tt, er, el = ref.step(ho, hr, hd, ht)
+        np.testing.assert_allclose(nobs.cpu().numpy(), o, rtol=1e-6, atol=1e-6, err_msg=f"obs @{t}")
+        np.testing.assert_allclose(nrew.cpu().numpy(), r, rtol=1e-6, atol=1e-6, err_msg=f"reward @{t}")
+        m = hd.astype(bool)
+        n_done += int(m.sum())
+        if m.any():
+            np.testing.assert_allclose(nterm.cpu().numpy()[m], tt[m], rtol=1e-6, atol=1e-6, err_msg=f"terminal obs @{t}")
+            np.testing.assert_array_equal(epr.cpu().numpy()[m], er[m], err_msg=f"episode return @{t}")
+            np.testing.assert_array_equal(epl.cpu().numpy()[m], el[m], err_msg=f"episode length @{t}")
+    assert n_done >= 2 * lanes
+    st = norm.get_stats()
+    np.testing.assert_allclose(st["obs_mean"], ref.obs_rms.mean, rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(st["obs_var"], ref.obs_rms.var, rtol=1e-10)
+    np.testing.assert_allclose([st["obs_count"], st["ret_count"]], [ref.obs_rms.count, ref.ret_rms.count], rtol=1e-15)
+    np.testing.assert_allclose([st["ret_mean"], st["ret_var"]], [ref.ret_rms.mean, ref.ret_rms.var], rtol=1e-10)
+    # evaluation mode freezes the statistics; set/get round-trips them
+    norm.training = False
+    b.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), trunc.data_ptr(), 0, term.data_ptr())
+    norm.step(obs, rew, done, nobs, nrew, term, nterm, epr, epl)
+    st2 = norm.get_stats()
+    np.testing.assert_array_equal(st2["obs_mean"], st["obs_mean"])
+    norm.set_stats(st)
+    np.testing.assert_array_equal(norm.get_stats()["obs_var"], st["obs_var"])
+    norm.close()
+    b.close()
+
+
+@pytest.mark.gpu
+def test_vecnormalize_wrapper_sb3_surface(gpu_lib):
+    from gym_puzzles_amd import MultiRobotPuzzleVecEnv, MultiRobotPuzzleVecNormalize
+    env = MultiRobotPuzzleVecNormalize(MultiRobotPuzzleVecEnv("MultiRobotPuzzle-v0", 64, seed=5, max_episode_steps=20))
+    o = env.reset()
+    assert o.shape == (64, 28) and o.dtype == np.float32
+    rs = np.random.RandomState(1)
+    eps = 0
+    for _ in range(45):
+        o, r, d, infos = env.step(rs.uniform(-1, 1, size=(64, 6)).astype(np.float32))
+        assert np.all(np.abs(o) <= 10.0) and np.all(np.abs(r) <= 10.0)
+        for i in np.nonzero(d)[0]:
+            eps += 1
+            ep = infos[i]["episode"]
+            assert 1 <= ep["l"] <= 20 and infos[i]["terminal_observation"].shape == (28,)
+    assert eps >= 2 * 64
+    env.close()
