@@ -75,6 +75,8 @@ def main():
     ap.add_argument("--seed", type=int, default=17)
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the per-step gather to rank 0")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--vecnormalize", action="store_true",
+                    help="also run SB3 VecNormalize + Monitor statistics on the device every step (train.py:68,80-82)")
     args = ap.parse_args()
 
     import torch
@@ -114,11 +116,22 @@ def main():
     gather = StepGather(Shard(rank, world, L), O, dev) if distributed and not args.no_gather else None
 
     b.reset()   # device-RNG spawns for every lane (seeded by global lane id)
+    norm = None
+    if args.vecnormalize:
+        from gym_puzzles_amd import DeviceVecNormalize
+        norm = DeviceVecNormalize(L, O, local_rank)
+        term = torch.zeros((L, O), dtype=torch.float32, device=dev)
+        nobs, nrew, nterm = torch.zeros_like(obs), torch.zeros_like(rew), torch.zeros_like(term)
+        epr, epl = torch.zeros(L, dtype=torch.float64, device=dev), torch.zeros(L, dtype=torch.int32, device=dev)
+        norm.reset(torch.from_numpy(b.obs).to(dev), nobs)
 
     def one_step():
-        b.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), trunc.data_ptr())
+        b.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), trunc.data_ptr(), 0,
+                      0 if norm is None else term.data_ptr())
+        if norm is not None:
+            norm.step(obs, rew, done, nobs, nrew, term, nterm, epr, epl)
         if gather is not None:
-            gather(obs, rew, done)
+            gather(nobs if norm is not None else obs, nrew if norm is not None else rew, done)
 
     for _ in range(args.warmup):
         one_step()
@@ -132,10 +145,13 @@ def main():
     t0 = time.perf_counter()
     for k in range(K):
         ev[k][0].record(stream)
-        b.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), trunc.data_ptr())
+        b.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), trunc.data_ptr(), 0,
+                      0 if norm is None else term.data_ptr())
         ev[k][1].record(stream)
+        if norm is not None:
+            norm.step(obs, rew, done, nobs, nrew, term, nterm, epr, epl)
         if gather is not None:
-            gather(obs, rew, done)
+            gather(nobs if norm is not None else obs, nrew if norm is not None else rew, done)
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()
@@ -168,7 +184,8 @@ def main():
             "data": "synthetic: device-RNG random actions, device-RNG spawns (reference draw ranges)",
             "config": {"workload": f"{ENV_NAMES[args.env]}, {L} lanes/GPU, random actions, auto-reset",
                        "lanes_per_gpu": L, "global_lanes": world * L,
-                       "parallelism": f"lane-sharded x{world}" + ("" if world == 1 or args.no_gather else " + gather to rank 0/step")},
+                       "parallelism": f"lane-sharded x{world}" + ("" if world == 1 or args.no_gather else " + gather to rank 0/step"),
+                       "vecnormalize": bool(args.vecnormalize)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,

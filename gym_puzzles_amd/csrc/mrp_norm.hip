@@ -19,8 +19,8 @@
 // tolerance (tests/test_norm.py), not bitwise.  Monitor sums are bit-exact.
 //
 // Kernels: k_moments (one block per statistic column: the D obs columns, plus one block that
-// advances the per-lane discounted returns and takes their moments) and k_apply (one thread
-// per lane: normalised obs / terminal obs / reward, returns reset, Monitor accumulators).
+// advances the per-lane discounted returns and takes their moments) and k_apply (one thread per
+// obs element for the normalised obs / terminal obs; per lane: reward, returns reset, Monitor).
 // Both are tiny next to k_step; the statistics stay on the device between steps.
 #include <hip/hip_runtime.h>
 
@@ -97,28 +97,33 @@ __global__ __launch_bounds__(NT) void k_moments(const float* __restrict__ obs, i
     }
 }
 
-__global__ void k_count(double* obs_count, int L) { *obs_count += (double)L; }
-
+// one thread per obs element (coalesced rows) for obs / terminal obs; threads e < L also do lane
+// e's reward, discounted-return reset and Monitor accumulators; thread 0 advances the obs count
+// (k_moments read the pre-update count)
 __global__ __launch_bounds__(NT) void k_apply(const float* __restrict__ obs, const float* __restrict__ term, int L, int D,
                                               const double* __restrict__ obs_mean, const double* __restrict__ obs_var,
+                                              double* __restrict__ obs_count, int count_obs,
                                               const double* __restrict__ ret_stats, double clip_obs, double clip_rew, double eps,
                                               const float* __restrict__ reward, const uint8_t* __restrict__ done,
                                               double* __restrict__ returns, float* __restrict__ obs_out, float* __restrict__ term_out,
                                               float* __restrict__ reward_out, double* __restrict__ ep_ret, int* __restrict__ ep_len,
                                               double* __restrict__ ep_ret_out, int* __restrict__ ep_len_out, int step) {
-    const int l = blockIdx.x * NT + threadIdx.x;
-    if (l >= L) return;
-    const bool fin = step && done && done[l];
-    for (int j = 0; j < D; ++j) {
+    const int e = blockIdx.x * NT + threadIdx.x;
+    if (e == 0 && count_obs) *obs_count += (double)L;
+    if (e < L * D) {
+        const int l = e / D, j = e - l * D;
         const double sd = sqrt(obs_var[j] + eps);
-        double x = ((double)obs[(size_t)l * D + j] - obs_mean[j]) / sd;
-        obs_out[(size_t)l * D + j] = (float)fmin(fmax(x, -clip_obs), clip_obs);
-        if (fin && term && term_out) {
-            double y = ((double)term[(size_t)l * D + j] - obs_mean[j]) / sd;
-            term_out[(size_t)l * D + j] = (float)fmin(fmax(y, -clip_obs), clip_obs);
+        double x = ((double)obs[e] - obs_mean[j]) / sd;
+        obs_out[e] = (float)fmin(fmax(x, -clip_obs), clip_obs);
+        if (step && done && done[l] && term && term_out) {
+            double y = ((double)term[e] - obs_mean[j]) / sd;
+            term_out[e] = (float)fmin(fmax(y, -clip_obs), clip_obs);
         }
     }
+    if (e >= L) return;
+    const int l = e;
     if (!step) { returns[l] = 0.0; ep_ret[l] = 0.0; ep_len[l] = 0; return; }
+    const bool fin = done && done[l];
     const double r = (double)reward[l];
     if (reward_out) {
         double x = r / sqrt(ret_stats[1] + eps);
@@ -244,14 +249,11 @@ static int norm_launch(mrp_norm* n, const float* obs, const float* reward, const
         hipLaunchKernelGGL(k_moments, dim3(D + 1), dim3(NT), 0, n->stream, obs, L, D, reward, n->d_returns, n->gamma,
                            n->obs_mean(), n->obs_var(), n->obs_count(), n->ret_stats(), upd_obs, upd_ret);
         NCHK(n, hipGetLastError());
-        if (upd_obs) {
-            hipLaunchKernelGGL(k_count, dim3(1), dim3(1), 0, n->stream, n->obs_count(), L);
-            NCHK(n, hipGetLastError());
-        }
     }
-    hipLaunchKernelGGL(k_apply, dim3((L + NT - 1) / NT), dim3(NT), 0, n->stream, obs, term, L, D, n->obs_mean(), n->obs_var(),
-                       n->ret_stats(), n->clip_obs, n->clip_rew, n->eps, reward, done, n->d_returns, obs_out, term_out, reward_out,
-                       n->d_ep_ret, n->d_ep_len, ep_ret_out, ep_len_out, step);
+    const int nthreads = L * D > L ? L * D : L;
+    hipLaunchKernelGGL(k_apply, dim3((nthreads + NT - 1) / NT), dim3(NT), 0, n->stream, obs, term, L, D, n->obs_mean(),
+                       n->obs_var(), n->obs_count(), upd_obs, n->ret_stats(), n->clip_obs, n->clip_rew, n->eps, reward, done,
+                       n->d_returns, obs_out, term_out, reward_out, n->d_ep_ret, n->d_ep_len, ep_ret_out, ep_len_out, step);
     NCHK(n, hipGetLastError());
     return MRP_OK;
 }
