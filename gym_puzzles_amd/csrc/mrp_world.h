@@ -1154,7 +1154,16 @@ template <int ENV> struct World {
             __syncthreads();
             if (!sh.isl_go) break;
             const int nc = is.nc;
-            if (nc > 0 && nc <= 64) solver_velocity_lanes(is, sh.u.sol.vcs, 180);
+            if (nc > 0 && nc <= 64) {
+                // the lanes with the most contact updates set the kernel's duration: let their
+                // sweeps win the SIMD's issue arbitration over co-resident waves
+                const int ncu = __builtin_amdgcn_readfirstlane(nc);
+                if (ncu >= 6) __builtin_amdgcn_s_setprio(3);
+                else if (ncu >= 4) __builtin_amdgcn_s_setprio(2);
+                else if (ncu >= 2) __builtin_amdgcn_s_setprio(1);
+                solver_velocity_lanes(is, sh.u.sol.vcs, 180);
+                __builtin_amdgcn_s_setprio(0);
+            }
             else if (nc > 64 && tid == 0) for (int it = 0; it < 180; ++it) solver_velocity(is, sh.u.sol.vcs);
             __syncthreads();
             if (tid == 0) {
@@ -1577,7 +1586,11 @@ template <int ENV> struct World {
             __syncthreads();
             if (sh.toi_solve) {
                 const int nc = sh.isl.nc;
-                if (nc <= 64) solver_velocity_lanes(sh.isl, sh.u.sol.vcs, 180);
+                if (nc <= 64) {
+                    __builtin_amdgcn_s_setprio(2);   // a TOI event is on this lane's critical path
+                    solver_velocity_lanes(sh.isl, sh.u.sol.vcs, 180);
+                    __builtin_amdgcn_s_setprio(0);
+                }
                 else if (tid == 0) for (int i = 0; i < 180; ++i) solver_velocity(sh.isl, sh.u.sol.vcs);
                 __syncthreads();
                 if (tid == 0) toi_event_post();
