@@ -221,6 +221,7 @@ template <int ENV> struct World {
     const EnvTables& T;
     const EnvParams& P;
     const int tid;
+    int step_prio = 0;   // issue priority of this lane for the rest of the step (wave-uniform)
 
     __device__ __forceinline__ World(SH& s, const EnvTables& t, const EnvParams& p, int thread) : sh(s), S(s.S), L(s.lt), T(t), P(p), tid(thread) {}
 
@@ -646,6 +647,17 @@ template <int ENV> struct World {
             sh.cover[i] = ov ? 1 : 0;
             if (ov) collide_polygons(i, L.shape[fa], xf(L.fix_body[fa]), L.shape[fb], xf(L.fix_body[fb]));
         }
+        // touching contacts after this update decide how much solver work the lane has left: the
+        // contact-heavy lanes set the kernel's duration, so they take issue priority from here on
+        int touching = 0;
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + tid;
+            const bool t = i < n && sh.cover[i] && sh.u.col.tpc[i] > 0;
+            touching += __popcll(__ballot(t));
+        }
+        touching = __builtin_amdgcn_readfirstlane(touching);
+        step_prio = touching >= 4 ? 2 : (touching >= 2 ? 1 : 0);
+        set_prio(step_prio);
         __syncthreads();
         if (tid == 0) {
             for (int i = 0; i < n; ++i) {
@@ -655,6 +667,15 @@ template <int ENV> struct World {
             }
         }
         __syncthreads();
+    }
+
+    // wave issue priority (s_setprio takes an immediate); `level` must be wave-uniform
+    __device__ __forceinline__ static void set_prio(int level) {
+        level = __builtin_amdgcn_readfirstlane(level);
+        if (level >= 3) __builtin_amdgcn_s_setprio(3);
+        else if (level == 2) __builtin_amdgcn_s_setprio(2);
+        else if (level == 1) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
     }
 
     // ---------------------------------------------------------------- contact solver
@@ -1158,11 +1179,10 @@ template <int ENV> struct World {
                 // the lanes with the most contact updates set the kernel's duration: let their
                 // sweeps win the SIMD's issue arbitration over co-resident waves
                 const int ncu = __builtin_amdgcn_readfirstlane(nc);
-                if (ncu >= 6) __builtin_amdgcn_s_setprio(3);
-                else if (ncu >= 4) __builtin_amdgcn_s_setprio(2);
-                else if (ncu >= 2) __builtin_amdgcn_s_setprio(1);
+                const int lvl = ncu >= 6 ? 3 : (ncu >= 4 ? 2 : (ncu >= 2 ? 1 : 0));
+                set_prio(lvl > step_prio ? lvl : step_prio);
                 solver_velocity_lanes(is, sh.u.sol.vcs, 180);
-                __builtin_amdgcn_s_setprio(0);
+                set_prio(step_prio);
             }
             else if (nc > 64 && tid == 0) for (int it = 0; it < 180; ++it) solver_velocity(is, sh.u.sol.vcs);
             __syncthreads();
@@ -1587,9 +1607,9 @@ template <int ENV> struct World {
             if (sh.toi_solve) {
                 const int nc = sh.isl.nc;
                 if (nc <= 64) {
-                    __builtin_amdgcn_s_setprio(2);   // a TOI event is on this lane's critical path
+                    set_prio(2 > step_prio ? 2 : step_prio);   // a TOI event is on this lane's critical path
                     solver_velocity_lanes(sh.isl, sh.u.sol.vcs, 180);
-                    __builtin_amdgcn_s_setprio(0);
+                    set_prio(step_prio);
                 }
                 else if (tid == 0) for (int i = 0; i < 180; ++i) solver_velocity(sh.isl, sh.u.sol.vcs);
                 __syncthreads();
