@@ -34,6 +34,7 @@ EXPORTED = (
     "mrp_set_time_limit", "mrp_selftest_sincos", "mrp_debug_stamps", "mrp_debug_stamps_ext",
     "mrp_debug_trace", "mrp_norm_create", "mrp_norm_destroy", "mrp_norm_last_error", "mrp_norm_set_stream",
     "mrp_norm_set_training", "mrp_norm_reset_device", "mrp_norm_step_device", "mrp_norm_get_stats", "mrp_norm_set_stats",
+    "mrp_render", "mrp_render_device", "mrp_get_goals", "mrp_shapes",
 )
 
 _lib = None
@@ -80,6 +81,10 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.mrp_set_state.argtypes = [P, P]
     L.mrp_set_time_limit.argtypes = [P, i]
     L.mrp_selftest_sincos.argtypes = [i, P, P, P, i]
+    L.mrp_render.argtypes = [P, P, i, i, i, P]
+    L.mrp_render_device.argtypes = [P, P, i, i, i, P]
+    L.mrp_get_goals.argtypes = [P, P]
+    L.mrp_shapes.argtypes = [i, P, P, P, P]
     L.mrp_debug_stamps.argtypes = [i, P]
     L.mrp_norm_create.argtypes = [i, i, i, d, d, d, d, ctypes.POINTER(P)]
     L.mrp_norm_destroy.argtypes = [P]
@@ -107,6 +112,17 @@ def env_dims(env_id: int) -> dict:
         raise ValueError(f"unknown env_id {env_id}")
     keys = ("obs_dim", "act_dim", "n_draws", "n_agents", "n_blocks", "max_episode_steps")
     return dict(zip(keys, (v.value for v in vals)))
+
+
+def shapes(env_id: int) -> dict:
+    """Fixture geometry of an env (host-only; creation order, local vertices)."""
+    L = load()
+    n = ctypes.c_int32()
+    fb, cnt = np.zeros(16, np.int32), np.zeros(16, np.int32)
+    v = np.zeros((16, 8, 2), np.float32)
+    if L.mrp_shapes(env_id, ctypes.byref(n), _p(fb), _p(cnt), _p(v)) != MRP_OK:
+        raise ValueError(f"unknown env_id {env_id}")
+    return {"n_fix": n.value, "fix_body": fb[:n.value], "counts": cnt[:n.value], "verts": v[:n.value]}
 
 
 def _p(a):
@@ -218,6 +234,26 @@ class Batch:
         out = np.zeros((self.n_lanes, w), np.uint32)
         self._check(load().mrp_get_state(self._h, _p(out)))
         return out
+
+    def get_goals(self) -> np.ndarray:
+        """block_final_pos per lane: float64 [n_lanes, n_blocks, 3] (v0 px, v2 scaled units)."""
+        out = np.zeros((self.n_lanes, self.n_blocks, 3), np.float64)
+        self._check(load().mrp_get_goals(self._h, _p(out)))
+        return out
+
+    def render(self, lanes=None, width: int | None = None, height: int | None = None) -> np.ndarray:
+        """rgb_array frames of the selected lanes: uint8 [n, height, width, 3] (row 0 = top),
+        the reference's render(mode='rgb_array') (multi_robot_puzzle_00.py:528-592)."""
+        w0, h0 = (640, 480) if self.env_id <= 1 else (1440, 810)
+        width, height = width or w0, height or h0
+        sel = np.ascontiguousarray(np.arange(self.n_lanes) if lanes is None else np.atleast_1d(lanes), np.int32)
+        out = np.zeros((len(sel), height, width, 3), np.uint8)
+        self._check(load().mrp_render(self._h, _p(sel), len(sel), width, height, _p(out)))
+        return out
+
+    def render_device(self, d_lanes_ptr: int, n: int, width: int, height: int, d_rgb_ptr: int):
+        """Asynchronous render into a device buffer (e.g. a torch uint8 tensor's data_ptr())."""
+        self._check(load().mrp_render_device(self._h, ctypes.c_void_p(d_lanes_ptr), n, width, height, ctypes.c_void_p(d_rgb_ptr)))
 
     def set_state(self, state: np.ndarray):
         s = np.ascontiguousarray(state, np.uint32)

@@ -25,6 +25,8 @@ using namespace mrp;
 
 __constant__ EnvTables g_tables[5];
 
+#include "mrp_render.h"
+
 namespace {
 
 constexpr int BLOCK = 64;   // one wave per block: lanes of a block never wait on each other
@@ -601,6 +603,88 @@ int mrp_debug_trace(int device, uint32_t* out, int n_lanes) {
     (void)device; (void)out; (void)n_lanes;
     return MRP_E_STATE;
 #endif
+}
+
+
+// ------------------------------------------------------------------------------ rendering
+static int render_args(mrp_ctx* ctx, int W, int H, mrpr::RenderArgs& A) {
+    if (W <= 0 || H <= 0 || (int64_t)W * H > (1 << 24)) return MRP_E_ARG;
+    const bool v0 = ctx->env_id <= 1;
+    const double ww = v0 ? 640.0 / 30.0 : 1440.0 / 560.0, wh = v0 ? 480.0 / 30.0 : 810.0 / 560.0;
+    A.sx = (float)(ww / W); A.sy = (float)(wh / H);
+    A.lw_unit = v0 ? (float)(1.0 / 30.0) : (float)(1.0 / 560.0);
+    A.ring_r = (float)(ctx->params.scaled_epsilon / (560.0 / 1440.0));
+    A.goal_scale = v0 ? 1.0 / 30.0 : 1440.0 / 560.0;
+    return MRP_OK;
+}
+
+int mrp_render_device(mrp_ctx* ctx, const int32_t* d_lanes, int n, int width, int height, uint8_t* d_rgb) {
+    if (!ctx || !d_lanes || !d_rgb || n <= 0) return MRP_E_ARG;
+    if (!ctx->have_reset) { ctx->err = "mrp_render: call mrp_reset first"; return MRP_E_STATE; }
+    mrpr::RenderArgs A;
+    if (render_args(ctx, width, height, A) != MRP_OK) { ctx->err = "mrp_render: bad image size"; return MRP_E_ARG; }
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    dim3 grid((unsigned)((width * height + mrpr::RBLOCK - 1) / mrpr::RBLOCK), (unsigned)n);
+    DISPATCH(ctx->env_id, hipLaunchKernelGGL(mrpr::k_render<E>, grid, dim3(mrpr::RBLOCK), 0, ctx->stream, ctx->d_state,
+                                             d_lanes, ctx->n_lanes, width, height, A, d_rgb));
+    HIPCHK(ctx, hipGetLastError());
+    return MRP_OK;
+}
+
+int mrp_render(mrp_ctx* ctx, const int32_t* lanes, int n, int width, int height, uint8_t* rgb) {
+    if (!ctx || !lanes || !rgb || n <= 0 || width <= 0 || height <= 0) return MRP_E_ARG;
+    for (int i = 0; i < n; ++i)
+        if (lanes[i] < 0 || lanes[i] >= ctx->n_lanes) { ctx->err = "mrp_render: lane index out of range"; return MRP_E_ARG; }
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int32_t* dl = nullptr; uint8_t* dimg = nullptr;
+    const size_t img = (size_t)n * width * height * 3;
+    int rc = MRP_E_HIP;
+    if (hipMalloc(&dl, n * sizeof(int32_t)) == hipSuccess && hipMalloc(&dimg, img) == hipSuccess &&
+        hipMemcpyAsync(dl, lanes, n * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream) == hipSuccess) {
+        rc = mrp_render_device(ctx, dl, n, width, height, dimg);
+        if (rc == MRP_OK) {
+            rc = MRP_E_HIP;
+            if (hipMemcpyAsync(rgb, dimg, img, hipMemcpyDeviceToHost, ctx->stream) == hipSuccess &&
+                hipStreamSynchronize(ctx->stream) == hipSuccess)
+                rc = MRP_OK;
+        }
+    }
+    if (rc == MRP_E_HIP && ctx->err.empty()) ctx->err = "mrp_render: HIP allocation/copy failed";
+    if (dl) (void)hipFree(dl);
+    if (dimg) (void)hipFree(dimg);
+    return rc;
+}
+
+int mrp_get_goals(mrp_ctx* ctx, double* out) {
+    if (!ctx || !out) return MRP_E_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    double* d = nullptr;
+    const size_t bytes = (size_t)ctx->n_lanes * ctx->n_blocks * 3 * sizeof(double);
+    HIPCHK(ctx, hipMalloc(&d, bytes));
+    DISPATCH(ctx->env_id, hipLaunchKernelGGL(mrpr::k_goals<E>, dim3((ctx->n_lanes + 255) / 256), dim3(256), 0, ctx->stream,
+                                             ctx->d_state, ctx->n_lanes, d));
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d, bytes, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) { ctx->err = std::string("mrp_get_goals: ") + hipGetErrorString(e); return MRP_E_HIP; }
+    return MRP_OK;
+}
+
+int mrp_shapes(int env_id, int32_t* n_fix, int32_t* fix_body, int32_t* counts, float* verts) {
+    EnvTables t;
+    if (!build_tables(env_id, t) || !n_fix || !fix_body || !counts || !verts) return MRP_E_ARG;
+    *n_fix = t.n_fix;
+    for (int f = 0; f < MAXF; ++f) {
+        fix_body[f] = f < t.n_fix ? t.fix_body[f] : -1;
+        counts[f] = f < t.n_fix ? t.shape[f].count : 0;
+        for (int i = 0; i < MAX_POLY; ++i) {
+            const bool ok = f < t.n_fix && i < t.shape[f].count;
+            verts[(f * MAX_POLY + i) * 2] = ok ? t.shape[f].v[i].x : 0.0f;
+            verts[(f * MAX_POLY + i) * 2 + 1] = ok ? t.shape[f].v[i].y : 0.0f;
+        }
+    }
+    return MRP_OK;
 }
 
 int mrp_selftest_sincos(int device, const float* x, float* sin_out, float* cos_out, int n) {

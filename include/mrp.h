@@ -116,6 +116,22 @@ int mrp_state_words(int env_id);
 int mrp_get_state(mrp_ctx* ctx, uint32_t* out /* [n_lanes][state_words] */);
 int mrp_set_state(mrp_ctx* ctx, const uint32_t* in);
 
+/* rgb_array rendering, replacing render(mode='rgb_array') of
+ * gym_puzzles/envs/multi_robot_puzzle_00.py:528-592 and multi_robot_puzzle_02.py:590-661
+ * (_render_human_vision).  Renders the n selected lanes into uint8 RGB images
+ * [n][height][width][3], row 0 at the top (the reference's `arr[::-1]`, :598); the full-size
+ * viewport is 640x480 (v0) / 1440x810 (v2), other sizes resample the same scene.  The
+ * rasteriser is defined in gym_puzzles_amd/csrc/mrp_render.h.  _device: device pointers,
+ * asynchronous on the ctx stream; plain: host pointers, synchronous. */
+int mrp_render_device(mrp_ctx* ctx, const int32_t* d_lanes, int n, int width, int height, uint8_t* d_rgb);
+int mrp_render(mrp_ctx* ctx, const int32_t* lanes, int n, int width, int height, uint8_t* rgb);
+/* per lane block_final_pos (x, y, angle) per block, in the units of the reference's
+ * block_final_pos (v0 px, v2 scaled units): double [n_lanes][n_blocks][3] */
+int mrp_get_goals(mrp_ctx* ctx, double* out);
+/* host-only: the env's fixture geometry (creation order; local vertices, 16 fixtures x 8
+ * vertices x (x, y); unused entries 0 / fix_body -1) */
+int mrp_shapes(int env_id, int32_t* n_fix, int32_t* fix_body, int32_t* counts, float* verts);
+
 /* Device self-test of the glibc-faithful sinf/cosf used by every b2Rot::Set on the GPU:
  * evaluates them on device `device` for n host inputs (host output arrays). */
 int mrp_selftest_sincos(int device, const float* x, float* sin_out, float* cos_out, int n);
