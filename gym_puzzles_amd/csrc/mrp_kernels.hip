@@ -619,12 +619,13 @@ static int render_args(mrp_ctx* ctx, int W, int H, mrpr::RenderArgs& A) {
 }
 
 int mrp_render_device(mrp_ctx* ctx, const int32_t* d_lanes, int n, int width, int height, uint8_t* d_rgb) {
-    if (!ctx || !d_lanes || !d_rgb || n <= 0) return MRP_E_ARG;
+    if (!ctx || !d_lanes || !d_rgb || n <= 0 || n > 65535) return MRP_E_ARG;   // n is gridDim.y
     if (!ctx->have_reset) { ctx->err = "mrp_render: call mrp_reset first"; return MRP_E_STATE; }
     mrpr::RenderArgs A;
     if (render_args(ctx, width, height, A) != MRP_OK) { ctx->err = "mrp_render: bad image size"; return MRP_E_ARG; }
     HIPCHK(ctx, hipSetDevice(ctx->device));
-    dim3 grid((unsigned)((width * height + mrpr::RBLOCK - 1) / mrpr::RBLOCK), (unsigned)n);
+    const int per_block = mrpr::RBLOCK * mrpr::RPPT;
+    dim3 grid((unsigned)((width * height + per_block - 1) / per_block), (unsigned)n);
     DISPATCH(ctx->env_id, hipLaunchKernelGGL(mrpr::k_render<E>, grid, dim3(mrpr::RBLOCK), 0, ctx->stream, ctx->d_state,
                                              d_lanes, ctx->n_lanes, width, height, A, d_rgb));
     HIPCHK(ctx, hipGetLastError());

@@ -23,11 +23,14 @@ using namespace mrp;
 enum : int { P_POLY = 0, P_CIRCLE = 1, P_RING = 2, P_RECT = 3 };
 constexpr int MAXPRIM = 64;
 constexpr int RBLOCK = 256;
+constexpr int RPPT = 8;       // pixels per thread: one display-list build serves RBLOCK*RPPT pixels
+constexpr float BPAD = 1e-4f;   // >> f32 rounding of the exact tests at these coordinates (|x| < 22 m)
 
 struct Prim {
     int type, nv;
     uint32_t rgb;
     float a, b, c, d;          // circle: cx, cy, r^2 ; ring: cx, cy, rin^2, rout^2 ; rect: xlo, ylo, xhi, yhi
+    float bx0, by0, bx1, by1;  // conservative bounding box (padded by BPAD): culls before the exact test
     float vx[MAX_POLY], vy[MAX_POLY];
 };
 
@@ -52,16 +55,24 @@ __device__ inline void add_poly(Prim* P, int& n, const EnvTables& T, int f, floa
     Prim& q = P[n++];
     q.type = P_POLY; q.rgb = rgb; q.nv = T.shape[f].count;
     for (int i = 0; i < q.nv; ++i) xf_point(px, py, s, c, T.shape[f].v[i].x, T.shape[f].v[i].y, q.vx[i], q.vy[i]);
+    q.bx0 = q.bx1 = q.vx[0]; q.by0 = q.by1 = q.vy[0];
+    for (int i = 1; i < q.nv; ++i) {
+        q.bx0 = fminf(q.bx0, q.vx[i]); q.bx1 = fmaxf(q.bx1, q.vx[i]);
+        q.by0 = fminf(q.by0, q.vy[i]); q.by1 = fmaxf(q.by1, q.vy[i]);
+    }
+    q.bx0 -= BPAD; q.by0 -= BPAD; q.bx1 += BPAD; q.by1 += BPAD;
 }
 __device__ inline void add_circle(Prim* P, int& n, float x, float y, float r, uint32_t rgb) {
     #pragma clang fp contract(off)
     Prim& q = P[n++];
     q.type = P_CIRCLE; q.rgb = rgb; q.a = x; q.b = y; q.c = r * r; q.nv = 0;
+    q.bx0 = x - r - BPAD; q.bx1 = x + r + BPAD; q.by0 = y - r - BPAD; q.by1 = y + r + BPAD;
 }
 __device__ inline void add_rect(Prim* P, int& n, float xlo, float ylo, float xhi, float yhi, uint32_t rgb) {
     #pragma clang fp contract(off)
     Prim& q = P[n++];
     q.type = P_RECT; q.rgb = rgb; q.a = xlo; q.b = ylo; q.c = xhi; q.d = yhi; q.nv = 0;
+    q.bx0 = xlo; q.by0 = ylo; q.bx1 = xhi; q.by1 = yhi;
 }
 
 // Display list of one lane, in the reference's draw order.
@@ -87,6 +98,7 @@ __device__ int build_scene(const LaneState<ENV>& S, const EnvTables& T, const Re
             Prim& q = P[n++];
             const float h = 2.5f * A.lw_unit, ri = A.ring_r - h, ro = A.ring_r + h;
             q.type = P_RING; q.rgb = wall; q.a = fx; q.b = fy; q.c = ri * ri; q.d = ro * ro; q.nv = 0;
+            q.bx0 = fx - ro - BPAD; q.bx1 = fx + ro + BPAD; q.by0 = fy - ro - BPAD; q.by1 = fy + ro + BPAD;
         }
     }
     // drawlist = boundary + blocks + agents (:409 / _02.py:440); body.fixtures is head-inserted
@@ -120,6 +132,7 @@ __device__ int build_scene(const LaneState<ENV>& S, const EnvTables& T, const Re
 
 __device__ inline bool hit(const Prim& q, float x, float y) {
     #pragma clang fp contract(off)
+    if (x < q.bx0 || x > q.bx1 || y < q.by0 || y > q.by1) return false;
     switch (q.type) {
     case P_POLY: {
         for (int i = 0; i < q.nv; ++i) {
@@ -136,8 +149,8 @@ __device__ inline bool hit(const Prim& q, float x, float y) {
     }
 }
 
-// grid: (ceil(W*H / RBLOCK), n_sel).  One workgroup builds its lane's display list in LDS
-// (thread 0; <= 64 primitives), then every thread shades one pixel by walking the list from
+// grid: (ceil(W*H / (RBLOCK*RPPT)), n_sel).  One workgroup builds its lane's display list in LDS
+// (thread 0; <= 64 primitives), then every thread shades RPPT pixels (RBLOCK apart), each by walking the list from
 // the top (the last primitive drawn) and stopping at the first hit.  Output rows are written
 // as contiguous RGB bytes, so consecutive threads store consecutive 3-byte pixels.
 template <int ENV>
@@ -156,15 +169,17 @@ __global__ __launch_bounds__(RBLOCK) void k_render(const uint32_t* __restrict__ 
         }
     }
     __syncthreads();
-    const int pix = blockIdx.x * RBLOCK + threadIdx.x;
-    if (pix >= W * H) return;
-    const int r = pix / W, c = pix - r * W;
-    const float x = ((float)c + 0.5f) * A.sx, y = ((float)(H - 1 - r) + 0.5f) * A.sy;
-    uint32_t rgb = 0;   // background: black
-    for (int i = np - 1; i >= 0; --i)
-        if (hit(P[i], x, y)) { rgb = P[i].rgb; break; }
-    uint8_t* o = out + ((size_t)sel * W * H + pix) * 3;
-    o[0] = (uint8_t)(rgb & 255); o[1] = (uint8_t)((rgb >> 8) & 255); o[2] = (uint8_t)(rgb >> 16);
+    for (int k = 0; k < RPPT; ++k) {
+        const int pix = (blockIdx.x * RPPT + k) * RBLOCK + threadIdx.x;
+        if (pix >= W * H) return;
+        const int r = pix / W, c = pix - r * W;
+        const float x = ((float)c + 0.5f) * A.sx, y = ((float)(H - 1 - r) + 0.5f) * A.sy;
+        uint32_t rgb = 0;   // background: black
+        for (int i = np - 1; i >= 0; --i)
+            if (hit(P[i], x, y)) { rgb = P[i].rgb; break; }
+        uint8_t* o = out + ((size_t)sel * W * H + pix) * 3;
+        o[0] = (uint8_t)(rgb & 255); o[1] = (uint8_t)((rgb >> 8) & 255); o[2] = (uint8_t)(rgb >> 16);
+    }
 }
 
 template <int ENV>
