@@ -18,7 +18,9 @@ on the GPU and the class only moves one row of inputs/outputs.  For thousands of
 * ``step`` returns ``(obs float64[O], reward float, done bool, {})``; the TimeLimit is gym's
   wrapper's job (``make()`` adds it), so the kernel's own TimeLimit is off here;
 * v2 terminal steps before ``update_params()`` raise ``AttributeError`` (_02.py:554,560,578);
-* ``render()`` is not built yet and raises ``NotImplementedError``.
+* ``render(mode='rgb_array')`` returns the frame the GPU renderer draws from the lane state
+  (uint8 [H, W, 3], ``mrp_render``; scene of multi_robot_puzzle_00.py:528-592 /
+  _02.py:590-661); ``mode='human'`` needs a pyglet window, which this build does not open.
 """
 from __future__ import annotations
 
@@ -74,8 +76,12 @@ class _MRPBase:
             raise AttributeError(f"'{type(self).__name__}' object has no attribute '{name}'")
         return obs[0].astype(np.float64), float(rew[0]), bool(done[0]), {}
 
-    def render(self, mode="human"):
-        raise NotImplementedError("rendering is not built yet (SURVEY.md 8f-3)")
+    def render(self, mode="human", close=False):
+        if close:
+            return None
+        if mode != "rgb_array":
+            raise NotImplementedError("only mode='rgb_array' is rendered (no pyglet window in this build)")
+        return self._b.render([0])[0]
 
     def close(self):
         if getattr(self, "_b", None) is not None:

@@ -100,7 +100,8 @@ class MultiRobotPuzzleVecEnv:
         return [False] * len(self._indices(indices))
 
     def get_images(self):
-        raise NotImplementedError("rendering is not built yet (SURVEY.md 8f-3)")
+        """One rgb_array frame per env (SB3 VecEnv.get_images; frames from mrp_render)."""
+        return list(self._b.render())
 
     def _indices(self, indices):
         if indices is None:

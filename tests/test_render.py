@@ -92,3 +92,27 @@ def test_render_bad_lane(gpu_lib):
     b.reset()
     with pytest.raises(MrpError):
         b.render([5])
+
+
+@pytest.mark.gpu
+def test_env_render_rgb_array(gpu_lib):
+    """gym surface: env.render('rgb_array') -> uint8 [480, 640, 3] (the reference's viewport)."""
+    from gym_puzzles_amd.envs import make
+    env = make("MultiRobotPuzzle-v0")
+    env.reset()
+    frame = env.render(mode="rgb_array")
+    assert frame.shape == (480, 640, 3) and frame.dtype == np.uint8
+    assert (frame == np.array([58, 153, 255], np.uint8)).all(axis=2).any()   # the final point is visible
+    with pytest.raises(NotImplementedError):
+        env.render(mode="human")
+
+
+@pytest.mark.gpu
+def test_vec_env_get_images(gpu_lib):
+    """SB3 VecEnv.get_images (used by VecVideoRecorder): one frame per env."""
+    from gym_puzzles_amd.vec_env import MultiRobotPuzzleVecEnv
+    venv = MultiRobotPuzzleVecEnv("MultiRobotPuzzle-v2", 3, seed=3, max_episode_steps=25)
+    venv.reset()
+    imgs = venv.get_images()
+    assert len(imgs) == 3 and all(i.shape == (810, 1440, 3) for i in imgs)
+    venv.close()
