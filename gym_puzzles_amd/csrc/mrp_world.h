@@ -24,6 +24,10 @@ namespace mrp {
 
 constexpr int NULLN = -1;
 
+// v_writelane_b32 (clang exposes no builtin for it; the LLVM intrinsic is bound by name, so the
+// compiler still inserts the readlane -> writelane wait states itself)
+extern "C" __device__ int mrp_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
 // Diagnostic phase timing (build with -DMRP_STAMPS; never in the shipped build): thread 0 of
 // every lane accumulates s_memtime deltas per phase into g_stamps.
 #ifdef MRP_STAMPS
@@ -939,14 +943,19 @@ template <int ENV> struct World {
     // velocity in lane k.  The Gauss-Seidel order is unchanged (one contact after another): for
     // contact i every lane reads the two bodies' velocities with v_readlane and evaluates its own
     // contact's update from its own registers, lane i's result is kept (impulses by a lane select,
-    // velocities by v_readlane + lane select into the body lanes), so the iters x nc contact
+    // velocities by v_readlane + v_writelane into the body lanes), so the iters x nc contact
     // updates never wait on LDS.  Float operations and their order are those
     // of solver_velocity, so the result is bitwise identical.  Every thread of the wave calls it;
     // needs is.nc <= 64.
     __device__ __forceinline__ static float rdl(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
     __device__ __forceinline__ static int rdli(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
-    // lane l of `old` replaced by the (wave-uniform) x: one v_cmp + v_cndmask
-    __device__ __forceinline__ float wrl(float old, float x, int l) const { return tid == l ? x : old; }
+    // lane l of `old` replaced by the wave-uniform x (v_writelane_b32)
+    __device__ __forceinline__ static float wrl(float old, float x, int l) { return __int_as_float(mrp_writelane(__float_as_int(x), l, __float_as_int(old))); }
+    __device__ __forceinline__ static bool fsame(float a, float b) { return __float_as_uint(a) == __float_as_uint(b); }
+    // Early exit, exact: one sweep is a pure function of (body velocities, contact impulses), so
+    // once the state after sweep k equals the state after sweep k-2 bit for bit the sequence has
+    // period 1 or 2 from there on and the state after sweep `iters` is the state after sweep k
+    // whenever k and iters have the same parity.  The state is compared at exactly those k.
     __device__ __forceinline__ void solver_velocity_lanes(Isl& is, VC* vcs, int iters) {
         const int nc = is.nc;
         const VC& my = vcs[tid < nc ? tid : 0];   // lanes >= nc evaluate a copy of contact 0 and are never kept
@@ -961,8 +970,12 @@ template <int ENV> struct World {
         float ni0 = my.ni[0], ni1 = my.ni[1], ti0 = my.ti[0], ti1 = my.ti[1];
         const int bk = tid < is.nb ? tid : 0;
         float bvx = is.vvx[bk], bvy = is.vvy[bk], bw = is.vw[bk];
+        // state snapshot for the period check (taken at sweeps k with k = iters mod 2)
+        float sni0 = ni0, sni1 = ni1, sti0 = ti0, sti1 = ti1, sbx = bvx, sby = bvy, sbw = bw;
+        bool have = (iters & 1) == 0;   // the initial state is sweep 0
+        const int ncu = __builtin_amdgcn_readfirstlane(nc);
         for (int it = 0; it < iters; ++it) {
-            for (int i = 0; i < nc; ++i) {
+            for (int i = 0; i < ncu; ++i) {
                 // every lane evaluates ITS contact's update from contact i's body velocities;
                 // only lane i's result is kept (the Gauss-Seidel order is contact by contact)
                 const int ia = rdli(cia, i), ib = rdli(cib, i), pcount = rdli(cpc, i);
@@ -975,7 +988,7 @@ template <int ENV> struct World {
                 {   // friction, point 0
                     V2 rA = v2(rAx0, rAy0), rB = v2(rBx0, rBy0);
                     V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
-                    float vt = vdot(dv, tangent) - 0.0f;
+                    float vt = vdot(dv, tangent);
                     float lambda = tmass0 * (-vt);
                     float maxFriction = friction * ni0;
                     float newImpulse = fclamp(ti0 + lambda, -maxFriction, maxFriction);
@@ -990,7 +1003,7 @@ template <int ENV> struct World {
                 if (pcount == 2) {   // friction, point 1
                     V2 rA = v2(rAx1, rAy1), rB = v2(rBx1, rBy1);
                     V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
-                    float vt = vdot(dv, tangent) - 0.0f;
+                    float vt = vdot(dv, tangent);
                     float lambda = tmass1 * (-vt);
                     float maxFriction = friction * ni1;
                     float newImpulse = fclamp(ti1 + lambda, -maxFriction, maxFriction);
@@ -1024,23 +1037,21 @@ template <int ENV> struct World {
                     float vn1 = vdot(dv1, normal), vn2 = vdot(dv2, normal);
                     V2 b = v2(vn1 - vbias0, vn2 - vbias1);
                     b = vsub(b, v2(k0 * a.x + k2 * a.y, k1 * a.x + k3 * a.y));
-                    V2 x;
-                    bool ok = false;
-                    x = vneg(v2(nm0 * b.x + nm2 * b.y, nm1 * b.x + nm3 * b.y));
-                    if (x.x >= 0.0f && x.y >= 0.0f) ok = true;
-                    if (!ok) {
+                    // the block solver's case is decided by lane i's values (wave-uniform
+                    // branches); the other lanes follow lane i's case and are discarded
+                    V2 x = vneg(v2(nm0 * b.x + nm2 * b.y, nm1 * b.x + nm3 * b.y));
+                    bool ok = true;
+                    if (!(rdl(x.x, i) >= 0.0f && rdl(x.y, i) >= 0.0f)) {
                         x.x = -nmass0 * b.x; x.y = 0.0f;
                         vn2 = k1 * x.x + b.y;
-                        if (x.x >= 0.0f && vn2 >= 0.0f) ok = true;
-                    }
-                    if (!ok) {
-                        x.x = 0.0f; x.y = -nmass1 * b.y;
-                        vn1 = k2 * x.y + b.x;
-                        if (x.y >= 0.0f && vn1 >= 0.0f) ok = true;
-                    }
-                    if (!ok) {
-                        x.x = 0.0f; x.y = 0.0f; vn1 = b.x; vn2 = b.y;
-                        if (vn1 >= 0.0f && vn2 >= 0.0f) ok = true;
+                        if (!(rdl(x.x, i) >= 0.0f && rdl(vn2, i) >= 0.0f)) {
+                            x.x = 0.0f; x.y = -nmass1 * b.y;
+                            vn1 = k2 * x.y + b.x;
+                            if (!(rdl(x.y, i) >= 0.0f && rdl(vn1, i) >= 0.0f)) {
+                                x.x = 0.0f; x.y = 0.0f;
+                                ok = rdl(b.x, i) >= 0.0f && rdl(b.y, i) >= 0.0f;
+                            }
+                        }
                     }
                     if (ok) {
                         V2 d = vsub(x, a);
@@ -1053,10 +1064,17 @@ template <int ENV> struct World {
                     }
                 }
                 // lane i's results go to the lanes of bodies A and B (A first, as the reference stores)
-                const float nAx = rdl(vA.x, i), nAy = rdl(vA.y, i), nwA = rdl(wA, i);
-                const float nBx = rdl(vB.x, i), nBy = rdl(vB.y, i), nwB = rdl(wB, i);
-                bvx = wrl(bvx, nAx, ia); bvy = wrl(bvy, nAy, ia); bw = wrl(bw, nwA, ia);
-                bvx = wrl(bvx, nBx, ib); bvy = wrl(bvy, nBy, ib); bw = wrl(bw, nwB, ib);
+                bvx = wrl(bvx, rdl(vA.x, i), ia); bvy = wrl(bvy, rdl(vA.y, i), ia); bw = wrl(bw, rdl(wA, i), ia);
+                bvx = wrl(bvx, rdl(vB.x, i), ib); bvy = wrl(bvy, rdl(vB.y, i), ib); bw = wrl(bw, rdl(wB, i), ib);
+            }
+            if (((it + 1 - iters) & 1) == 0) {   // sweep it+1 has the parity of iters
+                if (have) {
+                    const bool same = fsame(ni0, sni0) && fsame(ni1, sni1) && fsame(ti0, sti0) && fsame(ti1, sti1) &&
+                                      fsame(bvx, sbx) && fsame(bvy, sby) && fsame(bw, sbw);
+                    if (__builtin_amdgcn_ballot_w64(!same) == 0) break;
+                }
+                sni0 = ni0; sni1 = ni1; sti0 = ti0; sti1 = ti1; sbx = bvx; sby = bvy; sbw = bw;
+                have = true;
             }
         }
         if (tid < is.nb) { is.vvx[tid] = bvx; is.vvy[tid] = bvy; is.vw[tid] = bw; }
