@@ -160,7 +160,37 @@ MRP_HD float g_cosf(float y) {
     return (y - y) / (y - y);
 }
 
-MRP_HD Rot rot(float angle) { Rot q; q.s = g_sinf(angle); q.c = g_cosf(angle); return q; }
+// b2Rot::Set(angle) = {sinf(angle), cosf(angle)}: g_sinf and g_cosf fused over one range
+// reduction (the reduction and the sign pick are the same function of the input in both, so
+// each result is bit-identical to its standalone routine).
+MRP_HD Rot rot(float y) {
+    Rot q;
+    double x = y;
+    int n;
+    const uint32_t t = abstop12(y);
+    if (t < abstop12(0x1.921FB6p-1f)) {
+        if (t < abstop12(0x1p-12f)) { q.s = y; q.c = 1.0f; return q; }
+        const double x2 = x * x;
+        q.s = sincos_poly(x, x2, false, 0);
+        q.c = sincos_poly(x, x2, false, 1);
+    } else if (t < abstop12(120.0f)) {
+        x = reduce_fast(x, &n);
+        const double s = sc_sign(n);
+        q.s = sincos_poly(x * s, x * x, (n & 2) != 0, n);
+        q.c = sincos_poly(x * s, x * x, (n & 2) != 0, n ^ 1);
+    } else if (t < abstop12(__builtin_inff())) {
+        const uint32_t xi = f2u(y);
+        const int sign = xi >> 31;
+        x = reduce_large(xi, &n);
+        const double s = sc_sign(n + sign);
+        q.s = sincos_poly(x * s, x * x, ((n + sign) & 2) != 0, n);
+        q.c = sincos_poly(x * s, x * x, ((n + sign) & 2) != 0, n ^ 1);
+    } else {
+        q.s = (y - y) / (y - y);
+        q.c = q.s;
+    }
+    return q;
+}
 
 // ---------------------------------------------------------------------------------------
 // Counter-based RNG for on-device resets and synthetic actions (pure integer SplitMix64

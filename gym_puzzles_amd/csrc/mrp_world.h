@@ -182,6 +182,7 @@ template <int ENV> struct Shared {
     // TOI scan bookkeeping
     int tn, np, toi_done, toi_fnc, toi_solve;
     float toi_dt;
+    int toiIA, toiIB;     // island indices of the TOI pair (position iterations)
     int tcand[C];
     int plan[C];          // per list position: -2 cached, >= 0 candidate index
     int pslot[C];
@@ -1081,6 +1082,100 @@ template <int ENV> struct World {
         if (tid < nc) { VC& o = vcs[tid]; o.ni[0] = ni0; o.ni[1] = ni1; o.ti[0] = ti0; o.ti[1] = ti1; }
     }
 
+    // ---------------------------------------------------------------- lane-distributed position iterations
+    // b2ContactSolver::SolvePositionConstraints (toi = false) or SolveTOIPositionConstraints
+    // (toi = true), repeated until the reference's exit test passes or `iters` passes have run,
+    // with the island held in VGPRs across the wave as in solver_velocity_lanes: contact i's
+    // constants in lane i, island body k's position (c, a) in lane k, contact by contact in
+    // Gauss-Seidel order with lane i's result kept.  The rotations come from a two-entry memo
+    // keyed by the angle's bit pattern (b2Rot::Set is a pure function of the angle, and a body
+    // with invI = 0 - the v0 agents, the walls - keeps its angle through every pass).  Returns
+    // the number of passes run (the reference's loop count).  Every thread calls it; nc <= 64.
+    struct RotMemo {
+        uint32_t k0 = 0u, k1 = 0u;   // +0.0f: b2Rot::Set(+0) = {+0, 1}
+        Rot q0 = {0.0f, 1.0f}, q1 = {0.0f, 1.0f};
+        bool next1 = false;
+        __device__ __forceinline__ Rot get(float angle) {
+            const uint32_t b = __float_as_uint(angle);
+            if (b == k0) return q0;
+            if (b == k1) return q1;
+            const Rot q = rot(angle);
+            if (next1) { k1 = b; q1 = q; } else { k0 = b; q0 = q; }
+            next1 = !next1;
+            return q;
+        }
+    };
+    __device__ __forceinline__ int solver_position_lanes(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB, int iters) {
+        const int nc = is.nc;
+        const int me = tid < nc ? tid : 0;   // lanes >= nc evaluate a copy of contact 0 and are never kept
+        const VC& vc = vcs[me];
+        const PC& pc = pcs[me];
+        const int cia = vc.iaI, cib = vc.ibI, cpc = pc.pointCount, ctype = pc.type;
+        float mA = vc.mA, iA = vc.iA, mB = vc.mB, iB = vc.iB;
+        if (toi) {
+            if (!(cia == toiA || cia == toiB)) { mA = 0.0f; iA = 0.0f; }
+            if (!(cib == toiA || cib == toiB)) { mB = 0.0f; iB = 0.0f; }
+        }
+        const float lcAx = pc.lcAx, lcAy = pc.lcAy, lcBx = pc.lcBx, lcBy = pc.lcBy;
+        const float lnx = pc.lnx, lny = pc.lny, lpx0 = pc.lpx0, lpy0 = pc.lpy0, radA = pc.rA, radB = pc.rB;
+        const float qx0 = pc.lpx[0], qy0 = pc.lpy[0], qx1 = pc.lpx[1], qy1 = pc.lpy[1];
+        const int bk = tid < is.nb ? tid : 0;
+        float bx = is.pcx[bk], by = is.pcy[bk], ba = is.pa[bk];
+        const float baum = toi ? TOI_BAUMGARTE : BAUMGARTE;
+        const float exitSep = toi ? -1.5f * LINEAR_SLOP : -3.0f * LINEAR_SLOP;
+        const int ncu = __builtin_amdgcn_readfirstlane(nc);
+        RotMemo memo;
+        int it = 0;
+        while (it < iters) {
+            ++it;
+            float minSep = 0.0f;   // wave-uniform: lane i's separations in contact/point order
+            for (int i = 0; i < ncu; ++i) {
+                const int ia = rdli(cia, i), ib = rdli(cib, i), pcount = rdli(cpc, i), type = rdli(ctype, i);
+                V2 cA = v2(rdl(bx, ia), rdl(by, ia)); float aA = rdl(ba, ia);
+                V2 cB = v2(rdl(bx, ib), rdl(by, ib)); float aB = rdl(ba, ib);
+                for (int j = 0; j < 2; ++j) {
+                    if (j == pcount) break;
+                    Xf xA, xB;
+                    xA.q = memo.get(rdl(aA, i)); xB.q = memo.get(rdl(aB, i));
+                    xA.p = vsub(cA, mul_rv(xA.q, v2(lcAx, lcAy)));
+                    xB.p = vsub(cB, mul_rv(xB.q, v2(lcBx, lcBy)));
+                    const V2 lp = j == 0 ? v2(qx0, qy0) : v2(qx1, qy1);
+                    V2 normal, point; float sep;
+                    if (type == MT_FACEA) {
+                        normal = mul_rv(xA.q, v2(lnx, lny));
+                        V2 planePoint = mul_xv(xA, v2(lpx0, lpy0));
+                        V2 clipPoint = mul_xv(xB, lp);
+                        sep = vdot(vsub(clipPoint, planePoint), normal) - radA - radB;
+                        point = clipPoint;
+                    } else {
+                        normal = mul_rv(xB.q, v2(lnx, lny));
+                        V2 planePoint = mul_xv(xB, v2(lpx0, lpy0));
+                        V2 clipPoint = mul_xv(xA, lp);
+                        sep = vdot(vsub(clipPoint, planePoint), normal) - radA - radB;
+                        point = clipPoint;
+                        normal = vneg(normal);
+                    }
+                    V2 rA = vsub(point, cA), rB = vsub(point, cB);
+                    minSep = fmin_(minSep, rdl(sep, i));
+                    float Cc = fclamp(baum * (sep + LINEAR_SLOP), -MAX_LINEAR_CORRECTION, 0.0f);
+                    float rnA = vcross(rA, normal), rnB = vcross(rB, normal);
+                    float K = mA + mB + iA * rnA * rnA + iB * rnB * rnB;
+                    float impulse = K > 0.0f ? -Cc / K : 0.0f;
+                    V2 Pv = vmul(impulse, normal);
+                    cA = vsub(cA, vmul(mA, Pv));
+                    aA -= iA * vcross(rA, Pv);
+                    cB = vadd(cB, vmul(mB, Pv));
+                    aB += iB * vcross(rB, Pv);
+                }
+                bx = wrl(bx, rdl(cA.x, i), ia); by = wrl(by, rdl(cA.y, i), ia); ba = wrl(ba, rdl(aA, i), ia);
+                bx = wrl(bx, rdl(cB.x, i), ib); by = wrl(by, rdl(cB.y, i), ib); ba = wrl(ba, rdl(aB, i), ib);
+            }
+            if (minSep >= exitSep) break;
+        }
+        if (tid < is.nb) { is.pcx[tid] = bx; is.pcy[tid] = by; is.pa[tid] = ba; }
+        return it;
+    }
+
     __device__ __forceinline__ void integrate_positions(Isl& is, float h) {
         for (int i = 0; i < is.nb; ++i) {
             V2 c = v2(is.pcx[i], is.pcy[i]); float a = is.pa[i];
@@ -1133,17 +1228,30 @@ template <int ENV> struct World {
             solver_warm_start(is, vcs);
         }
     }
-    __device__ __forceinline__ void island_post(Isl& is, float h, VC* vcs, PC* pcs) {
+    // thread 0, after the velocity sweeps: store the impulses, integrate positions
+    __device__ __forceinline__ void island_mid(Isl& is, float h, VC* vcs) {
         if (is.nc > 0) solver_store(is, vcs);
         integrate_positions(is, h);
-        if (is.nc > 0) {
-            for (int it = 0; it < 60; ++it) {
-                ++S.posIters;
-                if (solver_position(is, vcs, pcs, false, -1, -1)) break;
+    }
+    // position iterations (whole wave; thread 0 over LDS past 64 contacts), posIters counted as
+    // the reference's loop does
+    __device__ __forceinline__ void island_position(Isl& is, VC* vcs, PC* pcs, int nc) {
+        if (nc > 0 && nc <= 64) {
+            const int n = solver_position_lanes(is, vcs, pcs, false, -1, -1, 60);
+            if (tid == 0) S.posIters += n;
+        } else if (tid == 0) {
+            if (nc > 0) {
+                for (int it = 0; it < 60; ++it) {
+                    ++S.posIters;
+                    if (solver_position(is, vcs, pcs, false, -1, -1)) break;
+                }
+            } else {
+                ++S.posIters;   // an empty island's first position pass already reports solved
             }
-        } else {
-            ++S.posIters;   // an empty island's first position pass already reports solved
         }
+    }
+    // thread 0: positions and velocities back to the bodies
+    __device__ __forceinline__ void island_post(Isl& is) {
         for (int i = 0; i < is.nb; ++i) {
             int b = is.bodies[i];
             if (!is_dyn(b)) continue;   // static bodies are unchanged by construction (v = 0, invMass = 0)
@@ -1192,20 +1300,23 @@ template <int ENV> struct World {
             }
             __syncthreads();
             if (!sh.isl_go) break;
-            const int nc = is.nc;
+            const int nc = __builtin_amdgcn_readfirstlane(is.nc);
+            // the lanes with the most contact updates set the kernel's duration: let their
+            // sweeps win the SIMD's issue arbitration over co-resident waves
+            const int lvl = nc >= 6 ? 3 : (nc >= 4 ? 2 : (nc >= 2 ? 1 : 0));
             if (nc > 0 && nc <= 64) {
-                // the lanes with the most contact updates set the kernel's duration: let their
-                // sweeps win the SIMD's issue arbitration over co-resident waves
-                const int ncu = __builtin_amdgcn_readfirstlane(nc);
-                const int lvl = ncu >= 6 ? 3 : (ncu >= 4 ? 2 : (ncu >= 2 ? 1 : 0));
                 set_prio(lvl > step_prio ? lvl : step_prio);
                 solver_velocity_lanes(is, sh.u.sol.vcs, 180);
-                set_prio(step_prio);
             }
             else if (nc > 64 && tid == 0) for (int it = 0; it < 180; ++it) solver_velocity(is, sh.u.sol.vcs);
             __syncthreads();
+            if (tid == 0) island_mid(is, h, sh.u.sol.vcs);
+            __syncthreads();
+            island_position(is, sh.u.sol.vcs, sh.u.sol.pcs, nc);
+            if (nc > 0 && nc <= 64) set_prio(step_prio);
+            __syncthreads();
             if (tid == 0) {
-                island_post(is, h, sh.u.sol.vcs, sh.u.sol.pcs);
+                island_post(is);
                 for (int i = 0; i < is.nb; ++i) if (!is_dyn(is.bodies[i])) bflag &= ~(1u << is.bodies[i]);
                 --seed;
             }
@@ -1466,7 +1577,12 @@ template <int ENV> struct World {
             else { V2 c = center(b); is.pcx[i] = c.x; is.pcy[i] = c.y; is.pa[i] = 0.0f; is.vvx[i] = 0.0f; is.vvy[i] = 0.0f; is.vw[i] = 0.0f; }
         }
         solver_init(is, vcs, pcs, false, 1.0f);
-        for (int i = 0; i < 20; ++i) if (solver_position(is, vcs, pcs, true, toiA, toiB)) break;
+        sh.toiIA = toiA; sh.toiIB = toiB;
+        // the TOI position iterations run on the whole wave next (solve_toi_coop), then island_toi_mid
+    }
+    // thread 0, after the TOI position iterations: the pair's sweep start, velocity constraints
+    __device__ __forceinline__ void island_toi_mid(Isl& is, VC* vcs, PC* pcs) {
+        const int toiA = sh.toiIA, toiB = sh.toiIB;
         {
             int ba = is.bodies[toiA], bb = is.bodies[toiB];
             if (is_dyn(ba)) { S.c0x[ba] = is.pcx[toiA]; S.c0y[ba] = is.pcy[toiA]; S.a0[ba] = is.pa[toiA]; }
@@ -1623,9 +1739,17 @@ template <int ENV> struct World {
             if (tid == 0) { sh.toi_solve = 0; toi_event(dt); }
             __syncthreads();
             if (sh.toi_solve) {
-                const int nc = sh.isl.nc;
+                const int nc = __builtin_amdgcn_readfirstlane(sh.isl.nc);
                 if (nc <= 64) {
                     set_prio(2 > step_prio ? 2 : step_prio);   // a TOI event is on this lane's critical path
+                    solver_position_lanes(sh.isl, sh.u.sol.vcs, sh.u.sol.pcs, true, sh.toiIA, sh.toiIB, 20);
+                } else if (tid == 0) {
+                    for (int i = 0; i < 20; ++i) if (solver_position(sh.isl, sh.u.sol.vcs, sh.u.sol.pcs, true, sh.toiIA, sh.toiIB)) break;
+                }
+                __syncthreads();
+                if (tid == 0) island_toi_mid(sh.isl, sh.u.sol.vcs, sh.u.sol.pcs);
+                __syncthreads();
+                if (nc <= 64) {
                     solver_velocity_lanes(sh.isl, sh.u.sol.vcs, 180);
                     set_prio(step_prio);
                 }
