@@ -75,6 +75,9 @@ def main():
     ap.add_argument("--seed", type=int, default=17)
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the per-step gather to rank 0")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--later-window", type=int, default=200,
+                    help="diagnostic: also time this many steps starting near --later-start (0 = off; N=1 only)")
+    ap.add_argument("--later-start", type=int, default=500)
     ap.add_argument("--vecnormalize", action="store_true",
                     help="also run SB3 VecNormalize + Monitor statistics on the device every step (train.py:68,80-82)")
     args = ap.parse_args()
@@ -163,6 +166,25 @@ def main():
         elapsed, kern_ms = float(t[0]), float(t[1])
 
     toi, pos = b.counters() if rank == 0 else (0, 0)
+    # Diagnostics only (never `value`): per-launch spread of the timed window, and the rate over a
+    # later window of the same episodes (every lane spawned at step 0; the first tens of steps
+    # after a spawn carry most of the overlap resolution, so a window's rate depends on where it sits).
+    kts = np.array([s.elapsed_time(e) for s, e in ev])
+    later = None
+    if args.later_window > 0 and rank == 0 and not distributed:
+        skip = max(0, args.later_start - (args.warmup + K))
+        for _ in range(skip):
+            one_step()
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        s0.record(stream)
+        for _ in range(args.later_window):
+            one_step()
+        s1.record(stream)
+        torch.cuda.synchronize(dev)
+        first = args.warmup + K + skip + 1
+        later = {"steps_after_spawn": [first, first + args.later_window - 1],
+                 "env_steps_per_s": L * args.later_window / (s0.elapsed_time(s1) * 1e-3)}
     if rank == 0:
         total_steps = world * L * K
         value = total_steps / elapsed
@@ -191,8 +213,13 @@ def main():
                          "traffic": traffic,
                          "kernel": "k_step", "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_launch": algo_bytes,
-                         "note": "latency/VALU-bound sequential-impulse solver; HBM fraction reported as the north star asks"},
-            "diagnostics": {"toi_events_total": toi, "position_iterations_total": pos},
+                         "limiter": "latency: the serial Gauss-Seidel chains (velocity sweeps, position passes, TOI) of "
+                                    "the slowest lanes, one wave's VALU issue; not HBM and not MFMA",
+                         "note": "HBM fraction reported because the north star asks for it (SURVEY.md 8d)"},
+            "diagnostics": {"toi_events_total": toi, "position_iterations_total": pos,
+                            "timed_steps_after_spawn": [args.warmup + 1, args.warmup + K],
+                            "kernel_ms_min_median_max": [float(kts.min()), float(np.median(kts)), float(kts.max())],
+                            "later_window": later},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.env, L, args.seed)

@@ -29,11 +29,12 @@ ENV_IDS = {
 EXPORTED = (
     "mrp_env_dims", "mrp_create", "mrp_destroy", "mrp_last_error", "mrp_n_lanes", "mrp_env_id",
     "mrp_set_stream", "mrp_synchronize", "mrp_set_reward_params", "mrp_update_params", "mrp_update_goal",
-    "mrp_reset", "mrp_reset_device", "mrp_step", "mrp_step_device", "mrp_set_auto_reset",
-    "mrp_get_bodies", "mrp_get_flags", "mrp_counters", "mrp_state_words", "mrp_get_state", "mrp_set_state",
+    "mrp_reset", "mrp_reset_device", "mrp_step", "mrp_step_device", "mrp_step_ex", "mrp_step_device_ex",
+    "mrp_set_auto_reset", "mrp_set_seed",
+    "mrp_get_bodies", "mrp_get_flags", "mrp_get_faults", "mrp_counters", "mrp_state_words", "mrp_get_state", "mrp_set_state",
     "mrp_set_time_limit", "mrp_selftest_sincos", "mrp_debug_stamps", "mrp_debug_stamps_ext",
-    "mrp_debug_trace", "mrp_norm_create", "mrp_norm_destroy", "mrp_norm_last_error", "mrp_norm_set_stream",
-    "mrp_norm_set_training", "mrp_norm_reset_device", "mrp_norm_step_device", "mrp_norm_get_stats", "mrp_norm_set_stats",
+    "mrp_debug_trace", "mrp_debug_progress", "mrp_norm_create", "mrp_norm_destroy", "mrp_norm_last_error", "mrp_norm_set_stream",
+    "mrp_norm_set_training", "mrp_norm_reset_device", "mrp_norm_step_device", "mrp_norm_step_device_ex", "mrp_norm_get_stats", "mrp_norm_set_stats",
     "mrp_render", "mrp_render_device", "mrp_get_goals", "mrp_shapes",
 )
 
@@ -72,9 +73,13 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.mrp_reset_device.argtypes = [P, P, P, P, P]
     L.mrp_step.argtypes = [P, P, P, P, P, P, P, P]
     L.mrp_step_device.argtypes = [P, P, P, P, P, P, P, P]
+    L.mrp_step_ex.argtypes = [P, P, P, P, P, P, P, P, P]
+    L.mrp_step_device_ex.argtypes = [P, P, P, P, P, P, P, P, P]
+    L.mrp_set_seed.argtypes = [P, u64]
     L.mrp_set_auto_reset.argtypes = [P, i]
     L.mrp_get_bodies.argtypes = [P, P]
     L.mrp_get_flags.argtypes = [P, P]
+    L.mrp_get_faults.argtypes = [P, P]
     L.mrp_counters.argtypes = [P, P, P]
     L.mrp_state_words.argtypes = [i]
     L.mrp_get_state.argtypes = [P, P]
@@ -95,9 +100,11 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.mrp_norm_set_training.argtypes = [P, i]
     L.mrp_norm_reset_device.argtypes = [P, P, P]
     L.mrp_norm_step_device.argtypes = [P] * 10
+    L.mrp_norm_step_device_ex.argtypes = [P] * 11
     L.mrp_norm_get_stats.argtypes = [P, P]
     L.mrp_norm_set_stats.argtypes = [P, P]
-    for name, args in (("mrp_debug_stamps_ext", [i, P, P, P]), ("mrp_debug_trace", [i, P, i])):
+    for name, args in (("mrp_debug_stamps_ext", [i, P, P, P]), ("mrp_debug_trace", [i, P, i]),
+                       ("mrp_debug_progress", [i, ctypes.POINTER(P), i])):
         if hasattr(L, name):   # diagnostics: absent from older builds
             getattr(L, name).argtypes = args
     _lib = L
@@ -143,6 +150,7 @@ class Batch:
         self._h = h
         self.obs = np.zeros((n_lanes, self.obs_dim), np.float32)
         self.reward = np.zeros(n_lanes, np.float32)
+        self.reward64 = np.zeros(n_lanes, np.float64)   # the reference's Python-float rewards
         self.done = np.zeros(n_lanes, np.uint8)
         self.truncated = np.zeros(n_lanes, np.uint8)
         self.status = np.zeros(n_lanes, np.uint8)
@@ -196,13 +204,21 @@ class Batch:
     def step(self, actions=None, want_terminal_obs=False):
         a = None if actions is None else np.ascontiguousarray(actions, np.float32).reshape(self.n_lanes, self.act_dim)
         term = self.terminal_obs if want_terminal_obs else None
-        self._check(load().mrp_step(self._h, _p(a), _p(self.obs), _p(self.reward), _p(self.done), _p(self.truncated),
-                                    _p(self.status), _p(term)))
+        self._check(load().mrp_step_ex(self._h, _p(a), _p(self.obs), _p(self.reward), _p(self.reward64), _p(self.done),
+                                       _p(self.truncated), _p(self.status), _p(term)))
         return self.obs, self.reward, self.done, self.truncated
 
-    def step_device(self, d_actions, d_obs, d_reward=None, d_done=None, d_trunc=None, d_status=None, d_term=None):
-        """Asynchronous step on device pointers (ints, e.g. torch ``tensor.data_ptr()``)."""
-        self._check(load().mrp_step_device(self._h, d_actions, d_obs, d_reward, d_done, d_trunc, d_status, d_term))
+    def step_device(self, d_actions, d_obs, d_reward=None, d_done=None, d_trunc=None, d_status=None, d_term=None,
+                    d_reward64=None):
+        """Asynchronous step on device pointers (ints, e.g. torch ``tensor.data_ptr()``);
+        ``d_reward64`` optionally receives the float64 rewards."""
+        self._check(load().mrp_step_device_ex(self._h, d_actions, d_obs, d_reward, d_reward64, d_done, d_trunc, d_status,
+                                              d_term))
+
+    def set_seed(self, seed: int):
+        """Re-key the device RNG (later resets and synthetic actions); lanes, parameters, stream
+        and time limit are kept."""
+        self._check(load().mrp_set_seed(self._h, int(seed)))
 
     def set_time_limit(self, max_episode_steps: int):
         self._check(load().mrp_set_time_limit(self._h, int(max_episode_steps)))
@@ -221,6 +237,12 @@ class Batch:
     def flags(self) -> np.ndarray:
         out = np.zeros((self.n_lanes, self.n_agents + 1), np.int32)
         self._check(load().mrp_get_flags(self._h, _p(out)))
+        return out
+
+    def faults(self) -> np.ndarray:
+        """Per-lane loop-guard fault codes (0 = none; include/mrp.h mrp_get_faults)."""
+        out = np.zeros(self.n_lanes, np.int32)
+        self._check(load().mrp_get_faults(self._h, _p(out)))
         return out
 
     def counters(self):

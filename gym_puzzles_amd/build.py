@@ -52,5 +52,7 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
 if __name__ == "__main__":
     if "--stamps" in sys.argv:   # diagnostic per-phase timing build (tools/phase_profile.py)
         print(build(force=True, verbose=True, out=os.path.join(HERE, "libmrp_stamps.so"), defines=("MRP_STAMPS",)))
+    elif "--progress" in sys.argv:   # diagnostic hang-localisation build (tools/hang_probe.py)
+        print(build(force=True, verbose=True, out=os.path.join(HERE, "libmrp_progress.so"), defines=("MRP_PROGRESS",)))
     else:
         print(build(force="--force" in sys.argv, verbose=True))

@@ -131,7 +131,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_reset(uint32_t* state, int nl, con
 
 template <int ENV>
 __global__ __launch_bounds__(BLOCK, 4) void k_step(uint32_t* state, int nl, const float* actions, float* obs, float* reward,
-                                                uint8_t* done_out, uint8_t* trunc_out, uint8_t* status_out, float* term_obs,
+                                                double* reward64, uint8_t* done_out, uint8_t* trunc_out, uint8_t* status_out, float* term_obs,
                                                 EnvParams P, uint64_t seed, uint64_t lane_offset, int auto_reset,
                                                 int max_steps) {
     using D = Dims<ENV>;
@@ -164,6 +164,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_step(uint32_t* state, int nl, cons
         int d = sh.done, tr = 0;
         if (max_steps > 0 && sh.S.elapsed >= max_steps) { tr = !d; d = 1; }   // gym TimeLimit
         if (reward) reward[lane] = (float)sh.reward;
+        if (reward64) reward64[lane] = sh.reward;   // the reference's Python float
         if (done_out) done_out[lane] = (uint8_t)d;
         if (trunc_out) trunc_out[lane] = (uint8_t)tr;
         if (status_out) status_out[lane] = (uint8_t)sh.kind;
@@ -225,6 +226,14 @@ __global__ __launch_bounds__(BLOCK) void k_bodies(const uint32_t* state, int nl,
     }
 }
 
+template <int ENV>
+__global__ __launch_bounds__(256) void k_faults(const uint32_t* state, int nl, int32_t* out) {
+    const int lane = blockIdx.x * 256 + threadIdx.x;
+    if (lane >= nl) return;
+    const LaneState<ENV>& S = *reinterpret_cast<const LaneState<ENV>*>(state + (size_t)lane * lane_words<ENV>());
+    out[lane] = S.fault;
+}
+
 // ------------------------------------------------------------------------------ host side
 thread_local std::string g_create_error;
 
@@ -251,6 +260,7 @@ struct mrp_ctx {
     uint8_t* d_mask = nullptr;
     float* d_obs = nullptr;
     float* d_reward = nullptr;
+    double* d_reward64 = nullptr;
     uint8_t* d_done = nullptr;
     uint8_t* d_trunc = nullptr;
     uint8_t* d_status = nullptr;
@@ -309,8 +319,8 @@ void mrp_destroy(mrp_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    void* bufs[] = {ctx->d_state, ctx->d_draws, ctx->d_actions, ctx->d_mask, ctx->d_obs, ctx->d_reward, ctx->d_done,
-                    ctx->d_trunc, ctx->d_status, ctx->d_term, ctx->d_bodies, ctx->d_flags};
+    void* bufs[] = {ctx->d_state, ctx->d_draws, ctx->d_actions, ctx->d_mask, ctx->d_obs, ctx->d_reward, ctx->d_reward64,
+                    ctx->d_done, ctx->d_trunc, ctx->d_status, ctx->d_term, ctx->d_bodies, ctx->d_flags};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
@@ -359,6 +369,7 @@ int mrp_create(int env_id, int n_lanes, int device, uint64_t seed, uint64_t lane
         {(void**)&ctx->d_obs, nl * ctx->obs_dim * sizeof(float)},
         {(void**)&ctx->d_term, nl * ctx->obs_dim * sizeof(float)},
         {(void**)&ctx->d_reward, nl * sizeof(float)},
+        {(void**)&ctx->d_reward64, nl * sizeof(double)},
         {(void**)&ctx->d_done, nl},
         {(void**)&ctx->d_trunc, nl},
         {(void**)&ctx->d_status, nl},
@@ -461,36 +472,55 @@ int mrp_reset(mrp_ctx* ctx, const uint8_t* mask, const double* draws, const floa
     return MRP_OK;
 }
 
-int mrp_step_device(mrp_ctx* ctx, const float* d_actions, float* d_obs, float* d_reward, uint8_t* d_done, uint8_t* d_trunc,
-                    uint8_t* d_status, float* d_term) {
+int mrp_step_device_ex(mrp_ctx* ctx, const float* d_actions, float* d_obs, float* d_reward, double* d_reward64,
+                       uint8_t* d_done, uint8_t* d_trunc, uint8_t* d_status, float* d_term) {
     if (!ctx || !d_obs) return MRP_E_ARG;
     if (!ctx->have_reset) { ctx->err = "step() called before reset()"; return MRP_E_STATE; }
     HIPCHK(ctx, hipSetDevice(ctx->device));
     DISPATCH(ctx->env_id, hipLaunchKernelGGL(k_step<E>, dim3(grid_for(ctx->n_lanes)), dim3(BLOCK), 0, ctx->stream, ctx->d_state,
-                                             ctx->n_lanes, d_actions, d_obs, d_reward, d_done, d_trunc, d_status, d_term,
-                                             ctx->params, ctx->seed, ctx->lane_offset, ctx->auto_reset, ctx->time_limit));
+                                             ctx->n_lanes, d_actions, d_obs, d_reward, d_reward64, d_done, d_trunc, d_status,
+                                             d_term, ctx->params, ctx->seed, ctx->lane_offset, ctx->auto_reset,
+                                             ctx->time_limit));
     HIPCHK(ctx, hipGetLastError());
     return MRP_OK;
 }
 
-int mrp_step(mrp_ctx* ctx, const float* actions, float* obs, float* reward, uint8_t* done, uint8_t* trunc, uint8_t* status,
-             float* term) {
+int mrp_step_device(mrp_ctx* ctx, const float* d_actions, float* d_obs, float* d_reward, uint8_t* d_done, uint8_t* d_trunc,
+                    uint8_t* d_status, float* d_term) {
+    return mrp_step_device_ex(ctx, d_actions, d_obs, d_reward, nullptr, d_done, d_trunc, d_status, d_term);
+}
+
+int mrp_step_ex(mrp_ctx* ctx, const float* actions, float* obs, float* reward, double* reward64, uint8_t* done, uint8_t* trunc,
+                uint8_t* status, float* term) {
     if (!ctx || !obs) return MRP_E_ARG;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     size_t nl = (size_t)ctx->n_lanes;
     if (actions)
         HIPCHK(ctx, hipMemcpyAsync(ctx->d_actions, actions, nl * ctx->act_dim * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
-    int rc = mrp_step_device(ctx, actions ? ctx->d_actions : nullptr, ctx->d_obs, ctx->d_reward, ctx->d_done, ctx->d_trunc,
-                             ctx->d_status, term ? ctx->d_term : nullptr);
+    int rc = mrp_step_device_ex(ctx, actions ? ctx->d_actions : nullptr, ctx->d_obs, ctx->d_reward,
+                                reward64 ? ctx->d_reward64 : nullptr, ctx->d_done, ctx->d_trunc, ctx->d_status,
+                                term ? ctx->d_term : nullptr);
     if (rc) return rc;
     HIPCHK(ctx, hipMemcpyAsync(obs, ctx->d_obs, nl * ctx->obs_dim * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
     if (reward) HIPCHK(ctx, hipMemcpyAsync(reward, ctx->d_reward, nl * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    if (reward64) HIPCHK(ctx, hipMemcpyAsync(reward64, ctx->d_reward64, nl * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     if (done) HIPCHK(ctx, hipMemcpyAsync(done, ctx->d_done, nl, hipMemcpyDeviceToHost, ctx->stream));
     if (trunc) HIPCHK(ctx, hipMemcpyAsync(trunc, ctx->d_trunc, nl, hipMemcpyDeviceToHost, ctx->stream));
     if (status) HIPCHK(ctx, hipMemcpyAsync(status, ctx->d_status, nl, hipMemcpyDeviceToHost, ctx->stream));
     if (term)
         HIPCHK(ctx, hipMemcpyAsync(term, ctx->d_term, nl * ctx->obs_dim * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return MRP_OK;
+}
+
+int mrp_step(mrp_ctx* ctx, const float* actions, float* obs, float* reward, uint8_t* done, uint8_t* trunc, uint8_t* status,
+             float* term) {
+    return mrp_step_ex(ctx, actions, obs, reward, nullptr, done, trunc, status, term);
+}
+
+int mrp_set_seed(mrp_ctx* ctx, uint64_t seed) {
+    if (!ctx) return MRP_E_ARG;
+    ctx->seed = seed;   // keys every later device-RNG draw; lane state, params, stream and time limit are kept
     return MRP_OK;
 }
 
@@ -502,6 +532,18 @@ int mrp_get_bodies(mrp_ctx* ctx, float* out) {
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipMemcpyAsync(out, ctx->d_bodies, (size_t)ctx->n_lanes * 6 * (ctx->n_agents + ctx->n_blocks) * sizeof(float),
                                hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return MRP_OK;
+}
+
+int mrp_get_faults(mrp_ctx* ctx, int32_t* out) {
+    if (!ctx || !out) return MRP_E_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int32_t* d = (int32_t*)ctx->d_flags;   // [n_lanes][n_agents+1] >= n_lanes words
+    DISPATCH(ctx->env_id, hipLaunchKernelGGL(k_faults<E>, dim3((ctx->n_lanes + 255) / 256), dim3(256), 0, ctx->stream,
+                                             ctx->d_state, ctx->n_lanes, d));
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemcpyAsync(out, d, (size_t)ctx->n_lanes * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     return MRP_OK;
 }
@@ -558,6 +600,23 @@ int mrp_counters(mrp_ctx* ctx, int64_t* toi_events, int64_t* pos_iters) {
 }
 
 // Diagnostic builds only (-DMRP_STAMPS): per-phase thread-0 cycle totals since the last call.
+int mrp_debug_progress(int device, uint32_t** host_words, int n_lanes) {
+#ifdef MRP_PROGRESS
+    if (!host_words || n_lanes <= 0 || hipSetDevice(device) != hipSuccess) return MRP_E_HIP;
+    uint32_t* h = nullptr;
+    if (hipHostMalloc((void**)&h, (size_t)n_lanes * 4, hipHostMallocMapped) != hipSuccess) return MRP_E_HIP;
+    for (int i = 0; i < n_lanes; ++i) h[i] = 0u;
+    uint32_t* d = nullptr;
+    if (hipHostGetDevicePointer((void**)&d, h, 0) != hipSuccess) return MRP_E_HIP;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_progress), &d, sizeof(d)) != hipSuccess) return MRP_E_HIP;
+    *host_words = h;
+    return MRP_OK;
+#else
+    (void)device; (void)host_words; (void)n_lanes;
+    return MRP_E_STATE;
+#endif
+}
+
 int mrp_debug_stamps(int device, uint64_t* out16) {
 #ifdef MRP_STAMPS
     if (!out16 || hipSetDevice(device) != hipSuccess) return MRP_E_HIP;

@@ -104,8 +104,8 @@ __global__ __launch_bounds__(NT) void k_apply(const float* __restrict__ obs, con
                                               const double* __restrict__ obs_mean, const double* __restrict__ obs_var,
                                               double* __restrict__ obs_count, int count_obs,
                                               const double* __restrict__ ret_stats, double clip_obs, double clip_rew, double eps,
-                                              const float* __restrict__ reward, const uint8_t* __restrict__ done,
-                                              double* __restrict__ returns, float* __restrict__ obs_out, float* __restrict__ term_out,
+                                              const float* __restrict__ reward, const double* __restrict__ reward64,
+                                              const uint8_t* __restrict__ done, double* __restrict__ returns, float* __restrict__ obs_out, float* __restrict__ term_out,
                                               float* __restrict__ reward_out, double* __restrict__ ep_ret, int* __restrict__ ep_len,
                                               double* __restrict__ ep_ret_out, int* __restrict__ ep_len_out, int step) {
     const int e = blockIdx.x * NT + threadIdx.x;
@@ -129,7 +129,8 @@ __global__ __launch_bounds__(NT) void k_apply(const float* __restrict__ obs, con
         double x = r / sqrt(ret_stats[1] + eps);
         reward_out[l] = (float)fmin(fmax(x, -clip_rew), clip_rew);
     }
-    double er = ep_ret[l] + r;
+    // Monitor sums the env's own (float64) rewards when the step exported them
+    double er = ep_ret[l] + (reward64 ? reward64[l] : r);
     int el = ep_len[l] + 1;
     if (fin) {
         returns[l] = 0.0;
@@ -240,8 +241,8 @@ int mrp_norm_set_training(mrp_norm* n, int training) {
     return MRP_OK;
 }
 
-static int norm_launch(mrp_norm* n, const float* obs, const float* reward, const uint8_t* done, const float* term, float* obs_out,
-                       float* reward_out, float* term_out, double* ep_ret_out, int* ep_len_out, int step) {
+static int norm_launch(mrp_norm* n, const float* obs, const float* reward, const double* reward64, const uint8_t* done,
+                       const float* term, float* obs_out, float* reward_out, float* term_out, double* ep_ret_out, int* ep_len_out, int step) {
     NCHK(n, hipSetDevice(n->device));
     const int L = n->n_lanes, D = n->obs_dim;
     const int upd_obs = n->training, upd_ret = step && n->training;
@@ -252,21 +253,29 @@ static int norm_launch(mrp_norm* n, const float* obs, const float* reward, const
     }
     const int nthreads = L * D > L ? L * D : L;
     hipLaunchKernelGGL(k_apply, dim3((nthreads + NT - 1) / NT), dim3(NT), 0, n->stream, obs, term, L, D, n->obs_mean(),
-                       n->obs_var(), n->obs_count(), upd_obs, n->ret_stats(), n->clip_obs, n->clip_rew, n->eps, reward, done,
-                       n->d_returns, obs_out, term_out, reward_out, n->d_ep_ret, n->d_ep_len, ep_ret_out, ep_len_out, step);
+                       n->obs_var(), n->obs_count(), upd_obs, n->ret_stats(), n->clip_obs, n->clip_rew, n->eps, reward, reward64,
+                       done, n->d_returns, obs_out, term_out, reward_out, n->d_ep_ret, n->d_ep_len, ep_ret_out, ep_len_out, step);
     NCHK(n, hipGetLastError());
     return MRP_OK;
 }
 
 int mrp_norm_reset_device(mrp_norm* n, const float* d_obs, float* d_obs_out) {
     if (!n || !d_obs || !d_obs_out) return MRP_E_ARG;
-    return norm_launch(n, d_obs, nullptr, nullptr, nullptr, d_obs_out, nullptr, nullptr, nullptr, nullptr, 0);
+    return norm_launch(n, d_obs, nullptr, nullptr, nullptr, nullptr, d_obs_out, nullptr, nullptr, nullptr, nullptr, 0);
+}
+
+int mrp_norm_step_device_ex(mrp_norm* n, const float* d_obs, const float* d_reward, const double* d_reward64, const uint8_t* d_done,
+                            const float* d_term_obs, float* d_obs_out, float* d_reward_out, float* d_term_out, double* d_ep_return,
+                            int32_t* d_ep_len) {
+    if (!n || !d_obs || !d_reward || !d_done || !d_obs_out || !d_reward_out) return MRP_E_ARG;
+    return norm_launch(n, d_obs, d_reward, d_reward64, d_done, d_term_obs, d_obs_out, d_reward_out, d_term_out, d_ep_return,
+                       d_ep_len, 1);
 }
 
 int mrp_norm_step_device(mrp_norm* n, const float* d_obs, const float* d_reward, const uint8_t* d_done, const float* d_term_obs,
                          float* d_obs_out, float* d_reward_out, float* d_term_out, double* d_ep_return, int32_t* d_ep_len) {
-    if (!n || !d_obs || !d_reward || !d_done || !d_obs_out || !d_reward_out) return MRP_E_ARG;
-    return norm_launch(n, d_obs, d_reward, d_done, d_term_obs, d_obs_out, d_reward_out, d_term_out, d_ep_return, d_ep_len, 1);
+    return mrp_norm_step_device_ex(n, d_obs, d_reward, nullptr, d_done, d_term_obs, d_obs_out, d_reward_out, d_term_out,
+                                   d_ep_return, d_ep_len);
 }
 
 int mrp_norm_get_stats(mrp_norm* n, double* out) {

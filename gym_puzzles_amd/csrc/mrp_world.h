@@ -48,9 +48,27 @@ __device__ uint32_t g_trace[16384][16];         // last step per lane: phases 0-
         }                                                                                   \
     } while (0)
 #else
-#define MRP_STAMP(k) do {} while (0)
+#define MRP_STAMP(k) MRP_PROG(0x100u * ((k) + 1))
 #define MRP_TRACE(k, v) do {} while (0)
 #endif
+// Diagnostic hang localisation (build with -DMRP_PROGRESS; never in the shipped build): thread 0
+// of every lane stores the last progress point it reached into host-mapped memory, which a host
+// watchdog reads while a launch is still running (tools/hang_probe.py).
+#ifdef MRP_PROGRESS
+__device__ uint32_t* g_progress;
+#define MRP_PROG(k)                                                                                          \
+    do {                                                                                                     \
+        if (threadIdx.x == 0 && g_progress)                                                                  \
+            __hip_atomic_store(g_progress + blockIdx.x, (uint32_t)(k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
+    } while (0)
+#else
+#define MRP_PROG(k) do {} while (0)
+#endif
+// Loop guards: every loop whose trip count depends on lane data has a bound no valid world can
+// reach; a guard that trips records its code in LaneState::fault and leaves the loop, so a
+// corrupted lane finishes its step (and is reported by mrp_get_faults) instead of hanging the GPU.
+constexpr int MRP_FAULT_TREE_UP = 1, MRP_FAULT_TREE_DOWN = 2, MRP_FAULT_TREE_REMOVE = 3, MRP_FAULT_CONTACT_LIST = 4,
+              MRP_FAULT_ISLANDS = 5, MRP_FAULT_TOI_PASSES = 6, MRP_FAULT_PAIR_DECODE = 7, MRP_FAULT_DFS = 8;
 constexpr float LINEAR_SLOP = 0.005f;
 constexpr float AABB_EXT = 0.1f;
 constexpr float AABB_MUL = 2.0f;
@@ -104,7 +122,8 @@ template <int ENV> struct alignas(16) LaneState {   // 16-B granules: moved with
     uint32_t stepCounter;
     int elapsed, blks_in_place, prev_blks_in_place;
     int goal_contact[D::NA];
-    int wall_contact, pad1;
+    int wall_contact;
+    int fault;   // 0, or the MRP_FAULT_* code of a loop guard that tripped (no step may spin forever)
     double agent_dist[D::NA];
     double block_distance[D::NB];
     double goal[D::NB][3];
@@ -137,8 +156,8 @@ template <int NBODY, int C> struct IslT {
 struct SweepV { float lcx, lcy, c0x, c0y, cx, cy, a0, a, alpha0; };
 struct DProxy { const V2* v; int count; float radius; };
 struct SVert { V2 wA, wB, w; float a; int iA, iB; };
-struct Simplex { SVert v[3]; int count; };
-struct SCache { float metric; int count; int iA[3], iB[3]; };
+struct Simplex { SVert v0, v1, v2; int count; };
+struct SCache { float metric; int count; int iA0, iA1, iA2, iB0, iB1, iB2; };
 struct SepFn { int type; V2 lp, axis; };
 
 // Per-launch LDS copy of the env tables the step indexes with lane-varying indices (fixture
@@ -258,6 +277,12 @@ template <int ENV> struct World {
     }
     __device__ __forceinline__ void t_free(int id) { S.tpar[id] = S.freeList; S.th[id] = -1; S.tud[id] = -1; S.freeList = id; --S.nodeCount; }
     __device__ __forceinline__ bool t_leaf(int id) const { return S.tc1[id] == NULLN; }
+    // contact-list walk guard: a list holds at most C contacts
+    __device__ __forceinline__ bool list_ok(int& g) {
+        if (++g <= C) return true;
+        S.fault = MRP_FAULT_CONTACT_LIST;
+        return false;
+    }
     __device__ __forceinline__ void t_combine_into(int dst, int a, int b) {
         S.tlx[dst] = fmin_(S.tlx[a], S.tlx[b]); S.tly[dst] = fmin_(S.tly[a], S.tly[b]);
         S.thx[dst] = fmax_(S.thx[a], S.thx[b]); S.thy[dst] = fmax_(S.thy[a], S.thy[b]);
@@ -303,7 +328,8 @@ template <int ENV> struct World {
         return iA;
     }
     __device__ __forceinline__ void t_fix_upwards(int index) {
-        while (index != NULLN) {
+        for (int g = 0; index != NULLN; ++g) {
+            if (g > LS::TN) { S.fault = MRP_FAULT_TREE_UP; break; }
             index = t_balance(index);
             int c1 = S.tc1[index], c2 = S.tc2[index];
             S.th[index] = 1 + max(S.th[c1], S.th[c2]);
@@ -315,7 +341,8 @@ template <int ENV> struct World {
         if (S.root == NULLN) { S.root = leaf; S.tpar[leaf] = NULLN; return; }
         float llx = S.tlx[leaf], lly = S.tly[leaf], lhx = S.thx[leaf], lhy = S.thy[leaf];
         int index = S.root;
-        while (!t_leaf(index)) {
+        for (int g = 0; !t_leaf(index); ++g) {
+            if (g > LS::TN) { S.fault = MRP_FAULT_TREE_DOWN; break; }
             int c1 = S.tc1[index], c2 = S.tc2[index];
             float area = perim(S.tlx[index], S.tly[index], S.thx[index], S.thy[index]);
             float combinedArea = perim(fmin_(S.tlx[index], llx), fmin_(S.tly[index], lly), fmax_(S.thx[index], lhx), fmax_(S.thy[index], lhy));
@@ -357,7 +384,8 @@ template <int ENV> struct World {
             S.tpar[sibling] = grand;
             t_free(parent);
             int index = grand;
-            while (index != NULLN) {   // RemoveLeaf: Combine before height (same result as t_fix_upwards)
+            for (int g = 0; index != NULLN; ++g) {   // RemoveLeaf: Combine before height (same result as t_fix_upwards)
+                if (g > LS::TN) { S.fault = MRP_FAULT_TREE_REMOVE; break; }
                 index = t_balance(index);
                 int c1 = S.tc1[index], c2 = S.tc2[index];
                 t_combine_into(index, c1, c2);
@@ -439,7 +467,7 @@ template <int ENV> struct World {
     __device__ __forceinline__ void add_pair(int fa, int fb) {   // b2ContactManager::AddPair
         int bA = L.fix_body[fa], bB = L.fix_body[fb];
         if (bA == bB) return;
-        for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
+        for (int c = S.cHead, g_ = 0; c != NULLN && list_ok(g_); c = S.cnext[c]) {
             if ((S.cfa[c] == fa && S.cfb[c] == fb) || (S.cfa[c] == fb && S.cfb[c] == fa)) return;
         }
         if (!is_dyn(bA) && !is_dyn(bB)) return;
@@ -483,7 +511,10 @@ template <int ENV> struct World {
         const int npairs = n * (n - 1) / 2;
         for (int p = tid; p < npairs; p += 64) {
             int i = 0, q = p;
-            while (q >= n - 1 - i) { q -= n - 1 - i; ++i; }
+            while (q >= n - 1 - i) {
+                if (i >= n - 1) { S.fault = MRP_FAULT_PAIR_DECODE; i = 0; q = 0; break; }
+                q -= n - 1 - i; ++i;
+            }
             int a = sh.prox[i], b = sh.prox[i + 1 + q];
             sh.u.pover[p] = ((((moved >> a) | (moved >> b)) & 1u) && fat_overlap(a, b)) ? 1 : 0;
         }
@@ -640,7 +671,7 @@ template <int ENV> struct World {
     __device__ __forceinline__ void collide_coop() {
         if (tid == 0) {
             int n = 0;
-            for (int c = S.cHead; c != NULLN; c = S.cnext[c]) sh.clist[n++] = c;
+            for (int c = S.cHead, g_ = 0; c != NULLN && list_ok(g_); c = S.cnext[c]) sh.clist[n++] = c;
             sh.ccount = n;
         }
         __syncthreads();
@@ -1269,8 +1300,10 @@ template <int ENV> struct World {
         Isl& is = sh.isl;
         uint32_t bflag = 0;   // body island flags (bit per body), thread 0
         int seed = ND - 1;    // next DFS seed, thread 0
-        if (tid == 0) for (int c = S.cHead; c != NULLN; c = S.cnext[c]) S.cflags[c] &= ~CF_ISLAND;
-        for (;;) {
+        if (tid == 0) for (int c = S.cHead, g_ = 0; c != NULLN && list_ok(g_); c = S.cnext[c]) S.cflags[c] &= ~CF_ISLAND;
+        for (int nisl = 0;; ++nisl) {
+            MRP_PROG(0x3000u + nisl);
+            if (nisl > NBODY + 1) { if (tid == 0) S.fault = MRP_FAULT_ISLANDS; break; }
             if (tid == 0) {
                 while (seed >= 0 && (bflag & (1u << seed))) --seed;
                 sh.isl_go = seed >= 0;
@@ -1279,11 +1312,12 @@ template <int ENV> struct World {
                     int* stack = sh.stack;
                     int sc = 0;
                     stack[sc++] = seed; bflag |= 1u << seed;
-                    while (sc > 0) {
+                    for (int g = 0; sc > 0; ++g) {
+                        if (g > 2 * NBODY) { S.fault = MRP_FAULT_DFS; break; }
                         int b = stack[--sc];
                         island_add_body(is, b);
                         if (!is_dyn(b)) continue;
-                        for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
+                        for (int c = S.cHead, g_ = 0; c != NULLN && list_ok(g_); c = S.cnext[c]) {
                             int bA = L.fix_body[S.cfa[c]], bB = L.fix_body[S.cfb[c]];
                             if (bA != b && bB != b) continue;
                             if (S.cflags[c] & CF_ISLAND) continue;
@@ -1310,11 +1344,14 @@ template <int ENV> struct World {
             }
             else if (nc > 64 && tid == 0) for (int it = 0; it < 180; ++it) solver_velocity(is, sh.u.sol.vcs);
             __syncthreads();
+            MRP_PROG(0x3400u + nisl);
             if (tid == 0) island_mid(is, h, sh.u.sol.vcs);
             __syncthreads();
+            MRP_PROG(0x3800u + nisl);
             island_position(is, sh.u.sol.vcs, sh.u.sol.pcs, nc);
             if (nc > 0 && nc <= 64) set_prio(step_prio);
             __syncthreads();
+            MRP_PROG(0x3c00u + nisl);
             if (tid == 0) {
                 island_post(is);
                 for (int i = 0; i < is.nb; ++i) if (!is_dyn(is.bodies[i])) bflag &= ~(1u << is.bodies[i]);
@@ -1364,22 +1401,30 @@ template <int ENV> struct World {
         for (int i = 1; i < p.count; ++i) { float val = vdot(p.v[i], d); if (val > bv) { best = i; bv = val; } }
         return best;
     }
+    // GJK simplex in named registers (an indexed array would live in scratch memory)
+    __device__ __forceinline__ static SVert make_vert(const DProxy& pA, Xf xA, const DProxy& pB, Xf xB, int iA, int iB) {
+        SVert v;
+        v.iA = iA; v.iB = iB;
+        v.wA = mul_xv(xA, pA.v[iA]); v.wB = mul_xv(xB, pB.v[iB]);
+        v.w = vsub(v.wB, v.wA); v.a = 0.0f;
+        return v;
+    }
     __device__ __forceinline__ static float s_metric(const Simplex& s) {
-        if (s.count == 2) return vlen(vsub(s.v[0].w, s.v[1].w));
-        if (s.count == 3) return vcross(vsub(s.v[1].w, s.v[0].w), vsub(s.v[2].w, s.v[0].w));
+        if (s.count == 2) return vlen(vsub(s.v0.w, s.v1.w));
+        if (s.count == 3) return vcross(vsub(s.v1.w, s.v0.w), vsub(s.v2.w, s.v0.w));
         return 0.0f;
     }
     __device__ __forceinline__ static void s_solve2(Simplex& s) {
-        V2 w1 = s.v[0].w, w2 = s.v[1].w, e12 = vsub(w2, w1);
+        V2 w1 = s.v0.w, w2 = s.v1.w, e12 = vsub(w2, w1);
         float d12_2 = -vdot(w1, e12);
-        if (d12_2 <= 0.0f) { s.v[0].a = 1.0f; s.count = 1; return; }
+        if (d12_2 <= 0.0f) { s.v0.a = 1.0f; s.count = 1; return; }
         float d12_1 = vdot(w2, e12);
-        if (d12_1 <= 0.0f) { s.v[1].a = 1.0f; s.count = 1; s.v[0] = s.v[1]; return; }
+        if (d12_1 <= 0.0f) { s.v1.a = 1.0f; s.count = 1; s.v0 = s.v1; return; }
         float inv = 1.0f / (d12_1 + d12_2);
-        s.v[0].a = d12_1 * inv; s.v[1].a = d12_2 * inv; s.count = 2;
+        s.v0.a = d12_1 * inv; s.v1.a = d12_2 * inv; s.count = 2;
     }
     __device__ __forceinline__ static void s_solve3(Simplex& s) {
-        V2 w1 = s.v[0].w, w2 = s.v[1].w, w3 = s.v[2].w;
+        V2 w1 = s.v0.w, w2 = s.v1.w, w3 = s.v2.w;
         V2 e12 = vsub(w2, w1);
         float d12_1 = vdot(w2, e12), d12_2 = -vdot(w1, e12);
         V2 e13 = vsub(w3, w1);
@@ -1388,73 +1433,71 @@ template <int ENV> struct World {
         float d23_1 = vdot(w3, e23), d23_2 = -vdot(w2, e23);
         float n123 = vcross(e12, e13);
         float d123_1 = n123 * vcross(w2, w3), d123_2 = n123 * vcross(w3, w1), d123_3 = n123 * vcross(w1, w2);
-        if (d12_2 <= 0.0f && d13_2 <= 0.0f) { s.v[0].a = 1.0f; s.count = 1; return; }
-        if (d12_1 > 0.0f && d12_2 > 0.0f && d123_3 <= 0.0f) { float inv = 1.0f / (d12_1 + d12_2); s.v[0].a = d12_1 * inv; s.v[1].a = d12_2 * inv; s.count = 2; return; }
-        if (d13_1 > 0.0f && d13_2 > 0.0f && d123_2 <= 0.0f) { float inv = 1.0f / (d13_1 + d13_2); s.v[0].a = d13_1 * inv; s.v[2].a = d13_2 * inv; s.count = 2; s.v[1] = s.v[2]; return; }
-        if (d12_1 <= 0.0f && d23_2 <= 0.0f) { s.v[1].a = 1.0f; s.count = 1; s.v[0] = s.v[1]; return; }
-        if (d13_1 <= 0.0f && d23_1 <= 0.0f) { s.v[2].a = 1.0f; s.count = 1; s.v[0] = s.v[2]; return; }
-        if (d23_1 > 0.0f && d23_2 > 0.0f && d123_1 <= 0.0f) { float inv = 1.0f / (d23_1 + d23_2); s.v[1].a = d23_1 * inv; s.v[2].a = d23_2 * inv; s.count = 2; s.v[0] = s.v[2]; return; }
+        if (d12_2 <= 0.0f && d13_2 <= 0.0f) { s.v0.a = 1.0f; s.count = 1; return; }
+        if (d12_1 > 0.0f && d12_2 > 0.0f && d123_3 <= 0.0f) { float inv = 1.0f / (d12_1 + d12_2); s.v0.a = d12_1 * inv; s.v1.a = d12_2 * inv; s.count = 2; return; }
+        if (d13_1 > 0.0f && d13_2 > 0.0f && d123_2 <= 0.0f) { float inv = 1.0f / (d13_1 + d13_2); s.v0.a = d13_1 * inv; s.v2.a = d13_2 * inv; s.count = 2; s.v1 = s.v2; return; }
+        if (d12_1 <= 0.0f && d23_2 <= 0.0f) { s.v1.a = 1.0f; s.count = 1; s.v0 = s.v1; return; }
+        if (d13_1 <= 0.0f && d23_1 <= 0.0f) { s.v2.a = 1.0f; s.count = 1; s.v0 = s.v2; return; }
+        if (d23_1 > 0.0f && d23_2 > 0.0f && d123_1 <= 0.0f) { float inv = 1.0f / (d23_1 + d23_2); s.v1.a = d23_1 * inv; s.v2.a = d23_2 * inv; s.count = 2; s.v0 = s.v2; return; }
         float inv = 1.0f / (d123_1 + d123_2 + d123_3);
-        s.v[0].a = d123_1 * inv; s.v[1].a = d123_2 * inv; s.v[2].a = d123_3 * inv; s.count = 3;
+        s.v0.a = d123_1 * inv; s.v1.a = d123_2 * inv; s.v2.a = d123_3 * inv; s.count = 3;
     }
     // b2Distance (GJK), returns distance between the (radius-free) cores
     __device__ __forceinline__ static float gjk(SCache& cache, const DProxy& pA, Xf xA, const DProxy& pB, Xf xB) {
         Simplex s;
         s.count = cache.count;
-        for (int i = 0; i < s.count; ++i) {
-            SVert& v = s.v[i];
-            v.iA = cache.iA[i]; v.iB = cache.iB[i];
-            v.wA = mul_xv(xA, pA.v[v.iA]); v.wB = mul_xv(xB, pB.v[v.iB]);
-            v.w = vsub(v.wB, v.wA); v.a = 0.0f;
-        }
+        s.v1.iA = s.v1.iB = s.v2.iA = s.v2.iB = -1;
+        if (s.count > 0) s.v0 = make_vert(pA, xA, pB, xB, cache.iA0, cache.iB0);
+        if (s.count > 1) s.v1 = make_vert(pA, xA, pB, xB, cache.iA1, cache.iB1);
+        if (s.count > 2) s.v2 = make_vert(pA, xA, pB, xB, cache.iA2, cache.iB2);
         if (s.count > 1) {
             float m1 = cache.metric, m2 = s_metric(s);
             if (m2 < 0.5f * m1 || 2.0f * m1 < m2 || m2 < FLT_EPS) s.count = 0;
         }
         if (s.count == 0) {
-            SVert& v = s.v[0];
-            v.iA = 0; v.iB = 0; v.wA = mul_xv(xA, pA.v[0]); v.wB = mul_xv(xB, pB.v[0]);
-            v.w = vsub(v.wB, v.wA); v.a = 1.0f; s.count = 1;
+            s.v0 = make_vert(pA, xA, pB, xB, 0, 0);
+            s.v0.a = 1.0f; s.count = 1;
         }
-        int saveA[3], saveB[3], saveCount;
         int iter = 0;
         while (iter < 20) {
-            saveCount = s.count;
-            for (int i = 0; i < saveCount; ++i) { saveA[i] = s.v[i].iA; saveB[i] = s.v[i].iB; }
+            const int saveCount = s.count;
+            const int sA0 = s.v0.iA, sB0 = s.v0.iB, sA1 = s.v1.iA, sB1 = s.v1.iB, sA2 = s.v2.iA, sB2 = s.v2.iB;
             if (s.count == 2) s_solve2(s); else if (s.count == 3) s_solve3(s);
             if (s.count == 3) break;
             V2 d;
-            if (s.count == 1) d = vneg(s.v[0].w);
+            if (s.count == 1) d = vneg(s.v0.w);
             else {
-                V2 e12 = vsub(s.v[1].w, s.v[0].w);
-                float sgn = vcross(e12, vneg(s.v[0].w));
+                V2 e12 = vsub(s.v1.w, s.v0.w);
+                float sgn = vcross(e12, vneg(s.v0.w));
                 d = sgn > 0.0f ? vcross_sv(1.0f, e12) : vcross_vs(e12, 1.0f);
             }
             if (vlensq(d) < FLT_EPS * FLT_EPS) break;
-            SVert& vt = s.v[s.count];
+            SVert vt;
             vt.iA = support(pA, mulT_rv(xA.q, vneg(d)));
             vt.wA = mul_xv(xA, pA.v[vt.iA]);
             vt.iB = support(pB, mulT_rv(xB.q, d));
             vt.wB = mul_xv(xB, pB.v[vt.iB]);
             vt.w = vsub(vt.wB, vt.wA);
+            vt.a = 0.0f;
             ++iter;
-            bool dup = false;
-            for (int i = 0; i < saveCount; ++i) if (vt.iA == saveA[i] && vt.iB == saveB[i]) { dup = true; break; }
+            const bool dup = (vt.iA == sA0 && vt.iB == sB0) || (saveCount > 1 && vt.iA == sA1 && vt.iB == sB1) ||
+                             (saveCount > 2 && vt.iA == sA2 && vt.iB == sB2);
             if (dup) break;
+            if (s.count == 1) s.v1 = vt; else s.v2 = vt;
             ++s.count;
         }
         V2 pa = v2(0.0f, 0.0f), pb = v2(0.0f, 0.0f);
-        if (s.count == 1) { pa = s.v[0].wA; pb = s.v[0].wB; }
+        if (s.count == 1) { pa = s.v0.wA; pb = s.v0.wB; }
         else if (s.count == 2) {
-            pa = vadd(vmul(s.v[0].a, s.v[0].wA), vmul(s.v[1].a, s.v[1].wA));
-            pb = vadd(vmul(s.v[0].a, s.v[0].wB), vmul(s.v[1].a, s.v[1].wB));
+            pa = vadd(vmul(s.v0.a, s.v0.wA), vmul(s.v1.a, s.v1.wA));
+            pb = vadd(vmul(s.v0.a, s.v0.wB), vmul(s.v1.a, s.v1.wB));
         } else if (s.count == 3) {
-            pa = vadd(vadd(vmul(s.v[0].a, s.v[0].wA), vmul(s.v[1].a, s.v[1].wA)), vmul(s.v[2].a, s.v[2].wA));
+            pa = vadd(vadd(vmul(s.v0.a, s.v0.wA), vmul(s.v1.a, s.v1.wA)), vmul(s.v2.a, s.v2.wA));
             pb = pa;
         }
         float dist = vlen(vsub(pa, pb));
         cache.metric = s_metric(s); cache.count = s.count;
-        for (int i = 0; i < s.count; ++i) { cache.iA[i] = s.v[i].iA; cache.iB[i] = s.v[i].iB; }
+        cache.iA0 = s.v0.iA; cache.iB0 = s.v0.iB; cache.iA1 = s.v1.iA; cache.iB1 = s.v1.iB; cache.iA2 = s.v2.iA; cache.iB2 = s.v2.iB;
         return dist;
     }
     __device__ __forceinline__ static float sep_eval(const SepFn& f, const DProxy& pA, const DProxy& pB, const SweepV& sA, const SweepV& sB, int iA, int iB, float t) {
@@ -1509,29 +1552,29 @@ template <int ENV> struct World {
             SepFn f;
             if (cache.count == 1) {
                 f.type = 0;
-                f.axis = vsub(mul_xv(xB, pB.v[cache.iB[0]]), mul_xv(xA, pA.v[cache.iA[0]]));
+                f.axis = vsub(mul_xv(xB, pB.v[cache.iB0]), mul_xv(xA, pA.v[cache.iA0]));
                 vnormalize(f.axis);
                 f.lp = v2(0.0f, 0.0f);
-            } else if (cache.iA[0] == cache.iA[1]) {
+            } else if (cache.iA0 == cache.iA1) {
                 f.type = 2;
-                V2 b1 = pB.v[cache.iB[0]], b2 = pB.v[cache.iB[1]];
+                V2 b1 = pB.v[cache.iB0], b2 = pB.v[cache.iB1];
                 f.axis = vcross_vs(vsub(b2, b1), 1.0f);
                 vnormalize(f.axis);
                 V2 normal = mul_rv(xB.q, f.axis);
                 f.lp = vmul(0.5f, vadd(b1, b2));
                 V2 pointB = mul_xv(xB, f.lp);
-                V2 pointA = mul_xv(xA, pA.v[cache.iA[0]]);
+                V2 pointA = mul_xv(xA, pA.v[cache.iA0]);
                 float s = vdot(vsub(pointA, pointB), normal);
                 if (s < 0.0f) f.axis = vneg(f.axis);
             } else {
                 f.type = 1;
-                V2 a1 = pA.v[cache.iA[0]], a2 = pA.v[cache.iA[1]];
+                V2 a1 = pA.v[cache.iA0], a2 = pA.v[cache.iA1];
                 f.axis = vcross_vs(vsub(a2, a1), 1.0f);
                 vnormalize(f.axis);
                 V2 normal = mul_rv(xA.q, f.axis);
                 f.lp = vmul(0.5f, vadd(a1, a2));
                 V2 pointA = mul_xv(xA, f.lp);
-                V2 pointB = mul_xv(xB, pB.v[cache.iB[0]]);
+                V2 pointB = mul_xv(xB, pB.v[cache.iB0]);
                 float s = vdot(vsub(pointB, pointA), normal);
                 if (s < 0.0f) f.axis = vneg(f.axis);
             }
@@ -1610,7 +1653,7 @@ template <int ENV> struct World {
     __device__ __forceinline__ void toi_scan() {
         float* salpha0 = sh.salpha0;
         int tn = 0, np = 0;
-        for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
+        for (int c = S.cHead, g_ = 0; c != NULLN && list_ok(g_); c = S.cnext[c]) {
             if ((S.cflags[c] & CF_ENABLED) == 0) continue;
             if (S.ctoiCount[c] > MAX_SUBSTEPS) continue;
             if (S.cflags[c] & CF_TOI) { sh.plan[np] = -2; sh.pslot[np++] = c; continue; }
@@ -1675,7 +1718,7 @@ template <int ENV> struct World {
         for (int k = 0; k < 2; ++k) {
             int body = pair[k];
             if (!is_dyn(body)) continue;
-            for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
+            for (int c = S.cHead, g_ = 0; c != NULLN && list_ok(g_); c = S.cnext[c]) {
                 int cA = L.fix_body[S.cfa[c]], cB = L.fix_body[S.cfb[c]];
                 if (cA != body && cB != body) continue;
                 if (is.nb == 2 * MAX_TOI_CONTACTS) break;
@@ -1710,7 +1753,7 @@ template <int ENV> struct World {
             int body = is.bodies[i];
             if (!is_dyn(body)) continue;
             sync_fixtures(body);
-            for (int c = S.cHead; c != NULLN; c = S.cnext[c]) {
+            for (int c = S.cHead, g_ = 0; c != NULLN && list_ok(g_); c = S.cnext[c]) {
                 int cA = L.fix_body[S.cfa[c]], cB = L.fix_body[S.cfb[c]];
                 if (cA == body || cB == body) S.cflags[c] &= ~(CF_TOI | CF_ISLAND);
             }
@@ -1721,10 +1764,12 @@ template <int ENV> struct World {
         if (tid == 0) {
             for (int i = 0; i < 4; ++i) sh.salpha0[i] = 0.0f;
             for (int b = 0; b < ND; ++b) S.alpha0[b] = 0.0f;
-            for (int c = S.cHead; c != NULLN; c = S.cnext[c]) { S.cflags[c] &= ~(CF_TOI | CF_ISLAND); S.ctoiCount[c] = 0; S.ctoi[c] = 1.0f; }
+            for (int c = S.cHead, g_ = 0; c != NULLN && list_ok(g_); c = S.cnext[c]) { S.cflags[c] &= ~(CF_TOI | CF_ISLAND); S.ctoiCount[c] = 0; S.ctoi[c] = 1.0f; }
             sh.toi_done = 0;
         }
-        for (;;) {
+        for (int pass = 0;; ++pass) {
+            MRP_PROG(0x2000u + pass);
+            if (pass > (MAX_SUBSTEPS + 1) * C + 2) { if (tid == 0) S.fault = MRP_FAULT_TOI_PASSES; break; }
             if (tid == 0) toi_scan();
             __syncthreads();
             const int tn = sh.tn;
@@ -1736,6 +1781,7 @@ template <int ENV> struct World {
                 sh.u.toi.tout[i] = time_of_impact(pA, pB, sh.u.toi.tsA[i], sh.u.toi.tsB[i]);
             }
             __syncthreads();
+            MRP_PROG(0x2800u + pass);
             if (tid == 0) { sh.toi_solve = 0; toi_event(dt); }
             __syncthreads();
             if (sh.toi_solve) {
@@ -1758,6 +1804,7 @@ template <int ENV> struct World {
                 if (tid == 0) toi_event_post();
                 __syncthreads();
             }
+            MRP_PROG(0x2c00u + pass);
             if (sh.toi_done) break;
             if (sh.toi_fnc) find_new_contacts_coop();
         }

@@ -27,7 +27,7 @@ from __future__ import annotations
 import numpy as np
 
 from ._native import STATUS_AGENT_OOB, STATUS_BLOCK_OOB, STATUS_PUZZLE_COMPLETE, Batch
-from .seeding import Box, np_random
+from .seeding import make_box, np_random
 from .spawn import reference_draws
 
 _DONE_STATUS = {STATUS_PUZZLE_COMPLETE: "puzzle complete!!", STATUS_AGENT_OOB: "agent out of bounds",
@@ -49,8 +49,8 @@ class _MRPBase:
         self.done_status = None
         self._params_updated = False
         self.set_reward_params()
-        self.observation_space = Box(-self._obs_high(), self._obs_high(), dtype=np.float32)
-        self.action_space = Box(-np.ones(self._b.act_dim), np.ones(self._b.act_dim), dtype=np.float32)
+        self.observation_space = make_box(-self._obs_high(), self._obs_high(), dtype=np.float32)
+        self.action_space = make_box(-np.ones(self._b.act_dim), np.ones(self._b.act_dim), dtype=np.float32)
         self.reset()
 
     # -- gym.Env API ---------------------------------------------------------------------
@@ -74,7 +74,7 @@ class _MRPBase:
             name = "shaped_bounds_penalty" if st == STATUS_AGENT_OOB else (
                 "shaped_blk_bounds_penalty" if st == STATUS_BLOCK_OOB else "shaped_puzzle_reward")
             raise AttributeError(f"'{type(self).__name__}' object has no attribute '{name}'")
-        return obs[0].astype(np.float64), float(rew[0]), bool(done[0]), {}
+        return obs[0].astype(np.float64), float(self._b.reward64[0]), bool(done[0]), {}
 
     def render(self, mode="human", close=False):
         if close:

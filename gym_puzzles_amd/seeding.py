@@ -113,3 +113,14 @@ class Box:
 
     def __repr__(self):
         return f"Box({self.low.min()}, {self.high.max()}, {self.shape}, {self.dtype})"
+
+
+def make_box(low, high, shape=None, dtype=np.float32):
+    """The env's observation/action space: ``gym.spaces.Box`` when gym is importable (SB3's
+    wrappers and policies dispatch on ``isinstance(space, gym.spaces.Box)``), else the numpy
+    restatement above (same bounds, dtype and sampling algorithm)."""
+    try:
+        from gym import spaces
+    except ImportError:
+        return Box(low, high, shape=shape, dtype=dtype)
+    return spaces.Box(low, high, shape=shape, dtype=dtype)

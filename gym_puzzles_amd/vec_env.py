@@ -11,19 +11,29 @@ seed and global lane), not from ``np.random``.
 
 ``step_torch`` is the zero-copy variant for a policy that lives on the same GPU: actions and
 outputs are torch CUDA tensors and nothing crosses PCIe.
+
+When stable-baselines3 is importable the class derives from its ``VecEnv`` and the spaces are
+``gym.spaces.Box`` (what SB3's wrappers check with ``isinstance``); neither package is in this
+image, so that path is untested here (parity unpinned) and ``MultiRobotPuzzleVecNormalize`` is
+the tested way to get VecNormalize + Monitor.
 """
 from __future__ import annotations
 
 import numpy as np
 
 from ._native import Batch, env_dims
-from .seeding import Box
+from .seeding import make_box
+
+try:   # SB3 1.x/2.x: VecEnv(num_envs, observation_space, action_space)
+    from stable_baselines3.common.vec_env.base_vec_env import VecEnv as _VecEnvBase
+except ImportError:
+    _VecEnvBase = object
 
 _ID = {"MultiRobotPuzzle-v0": 0, "MultiRobotPuzzleHeavy-v0": 1, "MultiRobotPuzzle-v2": 2,
        "MultiRobotPuzzleHeavy-v2": 3, "MultiRobotPuzzleHeavy-v2-3block": 4}
 
 
-class MultiRobotPuzzleVecEnv:
+class MultiRobotPuzzleVecEnv(_VecEnvBase):
     def __init__(self, env_id, num_envs: int, device: int = 0, seed: int = 0, lane_offset: int = 0,
                  max_episode_steps: int | None = None):
         self.env_index = _ID[env_id] if isinstance(env_id, str) else int(env_id)
@@ -32,8 +42,10 @@ class MultiRobotPuzzleVecEnv:
         self.device = device
         self._seed = seed
         self._lane_offset = lane_offset
-        self.observation_space = Box(-np.inf, np.inf, shape=(d["obs_dim"],), dtype=np.float32)
-        self.action_space = Box(-1.0, 1.0, shape=(d["act_dim"],), dtype=np.float32)
+        self.observation_space = make_box(-np.inf, np.inf, shape=(d["obs_dim"],), dtype=np.float32)
+        self.action_space = make_box(-1.0, 1.0, shape=(d["act_dim"],), dtype=np.float32)
+        if _VecEnvBase is not object:
+            _VecEnvBase.__init__(self, num_envs, self.observation_space, self.action_space)
         self.max_episode_steps = d["max_episode_steps"] if max_episode_steps is None else max_episode_steps
         self._b = None
         self._make_batch()
@@ -73,9 +85,10 @@ class MultiRobotPuzzleVecEnv:
             self._b = None
 
     def seed(self, seed=None):
-        """Re-key the device RNG (takes effect from the next reset); returns one seed per env."""
+        """Re-key the device RNG (takes effect from the next reset, as SB3's VecEnv.seed does);
+        lane state, tuning parameters, stream and time limit are kept.  Returns one seed per env."""
         self._seed = 0 if seed is None else int(seed)
-        self._make_batch()
+        self._b.set_seed(self._seed)
         return [self._seed + i for i in range(self.num_envs)]
 
     def get_attr(self, attr_name, indices=None):
@@ -111,15 +124,20 @@ class MultiRobotPuzzleVecEnv:
         return list(indices)
 
     # -- zero-copy device path -----------------------------------------------------------------
-    def step_torch(self, actions, obs, reward, done, truncated=None, terminal_obs=None):
-        """One step on torch CUDA tensors (float32 [N, A] actions, [N, O] obs, [N] reward,
-        uint8 [N] done/truncated, optional [N, O] terminal_obs), asynchronous on the current
-        torch stream."""
+    def step_torch(self, actions, obs, reward, done, truncated=None, terminal_obs=None, reward64=None):
+        """One step on torch CUDA tensors on this env's device (float32 [N, A] actions, [N, O] obs,
+        [N] reward, uint8 [N] done/truncated, optional [N, O] terminal_obs and float64 [N]
+        reward64), asynchronous on that device's current torch stream."""
         import torch
-        self._b.set_stream(torch.cuda.current_stream().cuda_stream)
+        dev = torch.device("cuda", self.device)
+        for name, t in (("actions", actions), ("obs", obs), ("reward", reward), ("done", done), ("truncated", truncated),
+                        ("terminal_obs", terminal_obs), ("reward64", reward64)):
+            if t is not None and t.device != dev:
+                raise ValueError(f"step_torch: {name} is on {t.device}, this VecEnv runs on {dev}")
+        self._b.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         ptr = (lambda t: 0 if t is None else t.data_ptr())
         self._b.step_device(ptr(actions), obs.data_ptr(), reward.data_ptr(), done.data_ptr(), ptr(truncated), 0,
-                            ptr(terminal_obs))
+                            ptr(terminal_obs), ptr(reward64))
 
     @property
     def batch(self) -> Batch:
@@ -167,11 +185,14 @@ class DeviceVecNormalize:
         self._sync_stream()
         self._check(self._L.mrp_norm_reset_device(self._h, obs.data_ptr(), obs_out.data_ptr()))
 
-    def step(self, obs, reward, done, obs_out, reward_out, term_obs=None, term_out=None, ep_return=None, ep_len=None):
+    def step(self, obs, reward, done, obs_out, reward_out, term_obs=None, term_out=None, ep_return=None, ep_len=None,
+             reward64=None):
+        """``reward64`` (float64 [N], optional): the env's float64 rewards, which Monitor's
+        episode return then sums (SB3's Monitor sums the env's Python-float rewards)."""
         ptr = (lambda t: None if t is None else t.data_ptr())
         self._sync_stream()
-        self._check(self._L.mrp_norm_step_device(self._h, ptr(obs), ptr(reward), ptr(done), ptr(term_obs), ptr(obs_out),
-                                                  ptr(reward_out), ptr(term_out), ptr(ep_return), ptr(ep_len)))
+        self._check(self._L.mrp_norm_step_device_ex(self._h, ptr(obs), ptr(reward), ptr(reward64), ptr(done), ptr(term_obs),
+                                                     ptr(obs_out), ptr(reward_out), ptr(term_out), ptr(ep_return), ptr(ep_len)))
 
     def get_stats(self) -> dict:
         st = np.zeros(2 * self.obs_dim + 4, np.float64)
@@ -218,6 +239,7 @@ class MultiRobotPuzzleVecNormalize:
         self._done, self._trunc, self._term = z(N, dt=torch.uint8), z(N, dt=torch.uint8), z(N, O)
         self._nobs, self._nrew, self._nterm = z(N, O), z(N), z(N, O)
         self._epr, self._epl = z(N, dt=torch.float64), z(N, dt=torch.int32)
+        self._rew64 = z(N, dt=torch.float64)
 
     @property
     def training(self):
@@ -236,8 +258,9 @@ class MultiRobotPuzzleVecNormalize:
     def step(self, actions):
         import torch
         self._act.copy_(torch.as_tensor(np.asarray(actions, np.float32).reshape(self.num_envs, -1)))
-        self.venv.step_torch(self._act, self._obs, self._rew, self._done, self._trunc, self._term)
-        self.norm.step(self._obs, self._rew, self._done, self._nobs, self._nrew, self._term, self._nterm, self._epr, self._epl)
+        self.venv.step_torch(self._act, self._obs, self._rew, self._done, self._trunc, self._term, self._rew64)
+        self.norm.step(self._obs, self._rew, self._done, self._nobs, self._nrew, self._term, self._nterm, self._epr, self._epl,
+                       self._rew64)
         obs, rew = self._nobs.cpu().numpy(), self._nrew.cpu().numpy()
         done, trunc = self._done.cpu().numpy().astype(bool), self._trunc.cpu().numpy().astype(bool)
         infos = [{} for _ in range(self.num_envs)]

@@ -99,7 +99,18 @@ int mrp_step(mrp_ctx* ctx, const float* actions, float* obs, float* reward, uint
              uint8_t* status, float* terminal_obs);
 int mrp_step_device(mrp_ctx* ctx, const float* d_actions, float* d_obs, float* d_reward, uint8_t* d_done,
                     uint8_t* d_truncated, uint8_t* d_status, float* d_terminal_obs);
+/* As mrp_step / mrp_step_device, plus `reward64` [n_lanes] float64 out (may be NULL): the reward
+ * exactly as the reference returns it (a Python float, multi_robot_puzzle_00.py:521,
+ * _02.py:584), before the float32 rounding of `reward`.  Monitor's episode return sums these. */
+int mrp_step_ex(mrp_ctx* ctx, const float* actions, float* obs, float* reward, double* reward64, uint8_t* done,
+                uint8_t* truncated, uint8_t* status, float* terminal_obs);
+int mrp_step_device_ex(mrp_ctx* ctx, const float* d_actions, float* d_obs, float* d_reward, double* d_reward64,
+                       uint8_t* d_done, uint8_t* d_truncated, uint8_t* d_status, float* d_terminal_obs);
 int mrp_set_auto_reset(mrp_ctx* ctx, int enabled);
+/* Re-key the device counter RNG (spawns of later resets, synthetic actions) without touching the
+ * lanes, parameters, stream or time limit: SB3 VecEnv.seed(seed) (train/train.py:63-75 seeds
+ * every env before the first reset).  Per-lane streams stay keyed by the global lane index. */
+int mrp_set_seed(mrp_ctx* ctx, uint64_t seed);
 /* TimeLimit max_episode_steps applied inside mrp_step (default: the registered value of
  * gym_puzzles/__init__.py:6-27); 0 disables it (when an outer gym.wrappers.TimeLimit is used). */
 int mrp_set_time_limit(mrp_ctx* ctx, int max_episode_steps);
@@ -109,6 +120,10 @@ int mrp_set_time_limit(mrp_ctx* ctx, int max_episode_steps);
 int mrp_get_bodies(mrp_ctx* ctx, float* out /* [n_lanes][6*(n_blocks+n_agents)] */);
 /* per lane: goal_contact flags [n_agents] then blks_in_place -> int32 [n_lanes][n_agents+1] */
 int mrp_get_flags(mrp_ctx* ctx, int32_t* out);
+/* per lane: 0, or the code of the loop guard that ended a runaway loop in that lane (a bound no
+ * valid world reaches: tree walks, contact-list walks, islands, TOI passes; see mrp_world.h
+ * MRP_FAULT_*).  Sticky.  int32 [n_lanes] */
+int mrp_get_faults(mrp_ctx* ctx, int32_t* out);
 /* summed over lanes: TOI events and position-solver iterations (diagnostics) */
 int mrp_counters(mrp_ctx* ctx, int64_t* toi_events, int64_t* pos_iters);
 /* Raw per-lane state (checkpoint / resume): mrp_state_words() 32-bit words per lane. */
@@ -145,6 +160,10 @@ int mrp_debug_stamps_ext(int device, uint64_t* pmax16, uint64_t* stepmax256, uin
 /* Diagnostic builds only: the last step's per-lane trace, n_lanes x 16 words (phase cycles 0-10,
  * total, island contacts, TOI events, position iterations, velocity-solver contact units). */
 int mrp_debug_trace(int device, uint32_t* out, int n_lanes);
+/* Diagnostic builds (-DMRP_PROGRESS) only: allocate n_lanes host-mapped words that every lane's
+ * thread 0 overwrites with the last progress point it reached; readable while a launch runs
+ * (hang localisation).  Returns MRP_E_STATE in the shipped build. */
+int mrp_debug_progress(int device, uint32_t** host_words, int n_lanes);
 
 /* ------------------------------------------------------------------------------------------
  * On-device VecNormalize + Monitor statistics.  Replaces the host-side
@@ -172,6 +191,11 @@ int mrp_norm_reset_device(mrp_norm* n, const float* d_obs, float* d_obs_out);
  * sum of raw rewards) and length (Monitor's info["episode"] r / l; optional outputs) */
 int mrp_norm_step_device(mrp_norm* n, const float* d_obs, const float* d_reward, const uint8_t* d_done, const float* d_term_obs,
                          float* d_obs_out, float* d_reward_out, float* d_term_out, double* d_ep_return, int32_t* d_ep_len);
+/* As mrp_norm_step_device; with d_reward64 (mrp_step_device_ex's float64 rewards, may be NULL) the
+ * Monitor episode return sums the env's float64 rewards, as SB3's Monitor does (train/train.py:68). */
+int mrp_norm_step_device_ex(mrp_norm* n, const float* d_obs, const float* d_reward, const double* d_reward64,
+                            const uint8_t* d_done, const float* d_term_obs, float* d_obs_out, float* d_reward_out,
+                            float* d_term_out, double* d_ep_return, int32_t* d_ep_len);
 /* statistics as float64[2*obs_dim + 4]: obs mean[obs_dim], obs var[obs_dim], obs count,
  * return mean, return var, return count (VecNormalize save/load) */
 int mrp_norm_get_stats(mrp_norm* n, double* out);

@@ -135,3 +135,43 @@ def test_vec_env_sb3_contract(gpu_lib):
     assert seen >= n * 2
     assert venv.env_method("update_params", 10, 1.01) == [None] * n
     venv.close()
+
+
+@pytest.mark.gpu
+def test_vec_env_seed_keeps_state_and_rekeys_resets(gpu_lib):
+    """seed() re-keys the device RNG for later resets without rebuilding the batch: tuning
+    parameters set through env_method survive and step() keeps working (SB3 VecEnv.seed)."""
+    from gym_puzzles_amd import MultiRobotPuzzleVecEnv
+    n = 32
+    a = MultiRobotPuzzleVecEnv("MultiRobotPuzzle-v0", n, seed=3)
+    b = MultiRobotPuzzleVecEnv("MultiRobotPuzzle-v0", n, seed=3)
+    oa, ob = a.reset(), b.reset()
+    assert np.array_equal(oa, ob)
+    a.env_method("set_reward_params", 10, 0.1, 50, 0.025)
+    assert a.seed(99) == [99 + i for i in range(n)]
+    act = np.zeros((n, 6), np.float32)
+    ra, rb = a.step(act), b.step(act)            # same lanes, same step: the re-key touches neither
+    assert np.array_equal(ra[0], rb[0]) and np.array_equal(ra[1], rb[1])
+    a.batch.reset(mask=np.ones(n, np.uint8))
+    assert not np.array_equal(a.batch.obs, b.reset())  # later resets draw from the new key
+    a.close()
+    b.close()
+
+
+@pytest.mark.gpu
+def test_step_torch_rejects_tensors_on_another_device(gpu_lib):
+    import torch
+
+    from gym_puzzles_amd import MultiRobotPuzzleVecEnv
+    n = 8
+    venv = MultiRobotPuzzleVecEnv("MultiRobotPuzzle-v0", n, seed=1)
+    venv.reset()
+    dev = torch.device("cuda", 0)
+    act, obs = torch.zeros((n, 6), device=dev), torch.zeros((n, 28), device=dev)
+    rew, done = torch.zeros(n, device=dev), torch.zeros(n, dtype=torch.uint8, device=dev)
+    with pytest.raises(ValueError):
+        venv.step_torch(act, obs, rew.cpu(), done)
+    venv.step_torch(act, obs, rew, done)
+    torch.cuda.synchronize(dev)
+    assert torch.isfinite(obs).all()
+    venv.close()

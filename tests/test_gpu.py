@@ -52,6 +52,12 @@ def test_step_parity_host_inputs(gpu_lib, orc, env_id):
         res = [o.step(a[l]) for l, o in enumerate(envs)]
         _eq(f"obs@{t}", obs, np.stack([r[0] for r in res]).astype(np.float32))
         _eq(f"reward@{t}", rew, np.array([r[1] for r in res]).astype(np.float32))
+        # float64 reward (the reference's Python float): the device takes distances with sqrt where
+        # CPython's `** 0.5` calls libm pow (1 ulp apart for ~0.1 % of inputs), so the float64 value
+        # carries a 1e-12 tolerance; its float32 rounding is the bit-exact `reward` above
+        r64 = np.array([r[1] for r in res], np.float64)
+        np.testing.assert_allclose(b.reward64, r64, rtol=1e-12, atol=1e-9, err_msg=f"reward64@{t}")
+        _eq(f"reward64->f32@{t}", b.reward64.astype(np.float32), rew)
         _eq(f"done@{t}", done, np.array([r[2] for r in res], np.uint8))
         _eq(f"status@{t}", b.status, np.array([r[3] for r in res], np.uint8))
         _eq(f"bodies@{t}", b.bodies(), np.stack([o.bodies() for o in envs]))
@@ -67,6 +73,7 @@ def test_step_parity_host_inputs(gpu_lib, orc, env_id):
     toi = sum(o.counters()[0] for o in envs)
     pos = sum(o.counters()[1] for o in envs)
     assert b.counters() == (toi, pos)
+    assert not b.faults().any(), "a loop guard tripped"
     b.close()
 
 
@@ -133,6 +140,7 @@ def test_device_autoreset_full_size(gpu_lib, orc, env_id):
     assert n_fin == int((eps - 1).sum()) and n_fin >= 3 * lanes
     _eq("bodies", b.bodies(), bodies)
     _eq("reward sums", rsum, orsum)
+    assert not b.faults().any(), "a loop guard tripped"
     b.close()
 
 

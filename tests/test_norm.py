@@ -117,3 +117,42 @@ def test_vecnormalize_wrapper_sb3_surface(gpu_lib):
             assert 1 <= ep["l"] <= 20 and infos[i]["terminal_observation"].shape == (28,)
     assert eps >= 2 * 64
     env.close()
+
+
+@pytest.mark.gpu
+def test_monitor_sums_the_float64_rewards(gpu_lib):
+    """Monitor's episode return sums the env's float64 rewards (SB3's Monitor sums the Python
+    floats step() returns), not their float32 roundings: mrp_step_device_ex's reward64 feeds
+    mrp_norm_step_device_ex, checked against a sequential float64 sum on the host."""
+    import torch
+
+    from gym_puzzles_amd import Batch, DeviceVecNormalize
+    lanes, steps = 256, 60
+    dev = torch.device("cuda", 0)
+    b = Batch(0, lanes, seed=8)
+    b.set_auto_reset(True)
+    b.set_time_limit(20)
+    O = b.obs_dim
+    norm = DeviceVecNormalize(lanes, O, 0)
+    obs0 = torch.from_numpy(b.reset().copy()).to(dev)
+    z = lambda *s, dt=torch.float32: torch.zeros(s, dtype=dt, device=dev)  # noqa: E731
+    nobs = torch.zeros_like(obs0)
+    norm.reset(obs0, nobs)
+    obs, rew, rew64, done = z(lanes, O), z(lanes), z(lanes, dt=torch.float64), z(lanes, dt=torch.uint8)
+    nrew, epr, epl = z(lanes), z(lanes, dt=torch.float64), z(lanes, dt=torch.int32)
+    b.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    acc = np.zeros(lanes, np.float64)
+    n_done = 0
+    for _ in range(steps):
+        b.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), 0, 0, 0, d_reward64=rew64.data_ptr())
+        norm.step(obs, rew, done, nobs, nrew, ep_return=epr, ep_len=epl, reward64=rew64)
+        r64, r32, d = rew64.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy().astype(bool)
+        np.testing.assert_array_equal(r64.astype(np.float32), r32)
+        acc = acc + r64
+        if d.any():
+            np.testing.assert_array_equal(epr.cpu().numpy()[d], acc[d])
+            acc[d] = 0.0
+            n_done += int(d.sum())
+    assert n_done >= 2 * lanes
+    norm.close()
+    b.close()
