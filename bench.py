@@ -75,6 +75,7 @@ def main():
     ap.add_argument("--seed", type=int, default=17)
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the per-step gather to rank 0")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--schedule", action="store_true", help="dispatch lanes costliest-first (mrp_set_schedule)")
     ap.add_argument("--later-window", type=int, default=200,
                     help="diagnostic: also time this many steps starting near --later-start (0 = off; N=1 only)")
     ap.add_argument("--later-start", type=int, default=500)
@@ -110,6 +111,7 @@ def main():
     torch.cuda.set_stream(stream)
     b.set_stream(stream.cuda_stream)
     b.set_auto_reset(True)
+    b.set_schedule(args.schedule)
     O = b.obs_dim
     obs = torch.zeros((L, O), dtype=torch.float32, device=dev)
     rew = torch.zeros(L, dtype=torch.float32, device=dev)

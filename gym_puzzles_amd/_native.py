@@ -30,10 +30,10 @@ EXPORTED = (
     "mrp_env_dims", "mrp_create", "mrp_destroy", "mrp_last_error", "mrp_n_lanes", "mrp_env_id",
     "mrp_set_stream", "mrp_synchronize", "mrp_set_reward_params", "mrp_update_params", "mrp_update_goal",
     "mrp_reset", "mrp_reset_device", "mrp_step", "mrp_step_device", "mrp_step_ex", "mrp_step_device_ex",
-    "mrp_set_auto_reset", "mrp_set_seed",
+    "mrp_set_auto_reset", "mrp_set_seed", "mrp_set_schedule",
     "mrp_get_bodies", "mrp_get_flags", "mrp_get_faults", "mrp_counters", "mrp_state_words", "mrp_get_state", "mrp_set_state",
     "mrp_set_time_limit", "mrp_selftest_sincos", "mrp_debug_stamps", "mrp_debug_stamps_ext",
-    "mrp_debug_trace", "mrp_debug_progress", "mrp_norm_create", "mrp_norm_destroy", "mrp_norm_last_error", "mrp_norm_set_stream",
+    "mrp_debug_trace", "mrp_debug_progress", "mrp_debug_velbench", "mrp_norm_create", "mrp_norm_destroy", "mrp_norm_last_error", "mrp_norm_set_stream",
     "mrp_norm_set_training", "mrp_norm_reset_device", "mrp_norm_step_device", "mrp_norm_step_device_ex", "mrp_norm_get_stats", "mrp_norm_set_stats",
     "mrp_render", "mrp_render_device", "mrp_get_goals", "mrp_shapes",
 )
@@ -76,6 +76,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.mrp_step_ex.argtypes = [P, P, P, P, P, P, P, P, P]
     L.mrp_step_device_ex.argtypes = [P, P, P, P, P, P, P, P, P]
     L.mrp_set_seed.argtypes = [P, u64]
+    L.mrp_set_schedule.argtypes = [P, i]
     L.mrp_set_auto_reset.argtypes = [P, i]
     L.mrp_get_bodies.argtypes = [P, P]
     L.mrp_get_flags.argtypes = [P, P]
@@ -104,7 +105,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.mrp_norm_get_stats.argtypes = [P, P]
     L.mrp_norm_set_stats.argtypes = [P, P]
     for name, args in (("mrp_debug_stamps_ext", [i, P, P, P]), ("mrp_debug_trace", [i, P, i]),
-                       ("mrp_debug_progress", [i, ctypes.POINTER(P), i])):
+                       ("mrp_debug_progress", [i, ctypes.POINTER(P), i]), ("mrp_debug_velbench", [i, i, i, i, i, P])):
         if hasattr(L, name):   # diagnostics: absent from older builds
             getattr(L, name).argtypes = args
     _lib = L
@@ -214,6 +215,10 @@ class Batch:
         ``d_reward64`` optionally receives the float64 rewards."""
         self._check(load().mrp_step_device_ex(self._h, d_actions, d_obs, d_reward, d_reward64, d_done, d_trunc, d_status,
                                               d_term))
+
+    def set_schedule(self, costliest_first: bool):
+        """Dispatch lanes costliest-first (default) or in lane order; results are identical."""
+        self._check(load().mrp_set_schedule(self._h, 1 if costliest_first else 0))
 
     def set_seed(self, seed: int):
         """Re-key the device RNG (later resets and synthetic actions); lanes, parameters, stream

@@ -133,12 +133,17 @@ template <int ENV>
 __global__ __launch_bounds__(BLOCK, 4) void k_step(uint32_t* state, int nl, const float* actions, float* obs, float* reward,
                                                 double* reward64, uint8_t* done_out, uint8_t* trunc_out, uint8_t* status_out, float* term_obs,
                                                 EnvParams P, uint64_t seed, uint64_t lane_offset, int auto_reset,
-                                                int max_steps) {
+                                                int max_steps, const int* __restrict__ order, uint32_t* __restrict__ cost) {
     using D = Dims<ENV>;
     __shared__ Shared<ENV> sh;
     __shared__ int s_fin;
-    const int lane = blockIdx.x, tid = threadIdx.x;
-    if (lane >= nl) return;
+    const int tid = threadIdx.x;
+    if ((int)blockIdx.x >= nl) return;
+    // workgroup b steps lane order[b]: the previous step's costliest lanes are dispatched first
+    // (k_order), so no SIMD collects several long serial chains; a lane's result does not depend
+    // on which workgroup steps it
+    const int lane = order ? order[blockIdx.x] : (int)blockIdx.x;
+    const unsigned long long t_start = cost ? __builtin_amdgcn_s_memtime() : 0ull;
     const uint64_t glane = lane_offset + lane;
 #ifdef MRP_STAMPS
     if (tid == 0) { sh.stamp_t = sh.stamp_t0 = __builtin_amdgcn_s_memtime(); sh.stamp_rt0 = __builtin_amdgcn_s_memrealtime(); }
@@ -182,10 +187,12 @@ __global__ __launch_bounds__(BLOCK, 4) void k_step(uint32_t* state, int nl, cons
     }
     for (int k = tid; k < D::OBS; k += BLOCK) orow[k] = sh.obs[k];
     store_state<ENV>(sh.S, state, lane, tid);
+    if (cost && tid == 0) cost[lane] = (uint32_t)min(__builtin_amdgcn_s_memtime() - t_start, 0xffffffffull);
     MRP_STAMP(10);
 #ifdef MRP_STAMPS
     if (tid == 0) {
         unsigned long long tot = sh.stamp_t - sh.stamp_t0;
+        for (int k = 0; k < 11; ++k) { atomicAdd(&g_stamps[k], (unsigned long long)sh.trace[k]); atomicMax(&g_pmax[k], (unsigned long long)sh.trace[k]); }
         atomicAdd(&g_rt[0], tot);
         atomicAdd(&g_rt[1], __builtin_amdgcn_s_memrealtime() - sh.stamp_rt0);
         atomicMax(&g_stepmax[(sh.S.stepCounter - 1u) & 255u], tot);
@@ -226,12 +233,84 @@ __global__ __launch_bounds__(BLOCK) void k_bodies(const uint32_t* state, int nl,
     }
 }
 
+// Dispatch order for the next step: lanes by descending cost of this step (counting sort over 64
+// linear buckets of [0, max cost]; order inside a bucket is arbitrary and never affects results).
+constexpr int ORDER_NT = 1024, ORDER_NB = 64;
+__global__ __launch_bounds__(ORDER_NT) void k_order(const uint32_t* __restrict__ cost, int nl, int* __restrict__ order) {
+    __shared__ uint32_t s_max;
+    __shared__ int s_cnt[ORDER_NB], s_base[ORDER_NB];
+    const int t = threadIdx.x;
+    if (t == 0) s_max = 1u;
+    if (t < ORDER_NB) s_cnt[t] = 0;
+    __syncthreads();
+    uint32_t m = 1u;
+    for (int l = t; l < nl; l += ORDER_NT) m = max(m, cost[l]);
+    atomicMax(&s_max, m);
+    __syncthreads();
+    const uint64_t mx = s_max;
+    for (int l = t; l < nl; l += ORDER_NT) {
+        const int b = (ORDER_NB - 1) - (int)(((uint64_t)cost[l] * (ORDER_NB - 1)) / mx);   // bucket 0 = costliest
+        atomicAdd(&s_cnt[b], 1);
+    }
+    __syncthreads();
+    if (t == 0) {
+        int acc = 0;
+        for (int b = 0; b < ORDER_NB; ++b) { s_base[b] = acc; acc += s_cnt[b]; }
+    }
+    __syncthreads();
+    for (int l = t; l < nl; l += ORDER_NT) {
+        const int b = (ORDER_NB - 1) - (int)(((uint64_t)cost[l] * (ORDER_NB - 1)) / mx);
+        order[atomicAdd(&s_base[b], 1)] = l;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_iota(int* __restrict__ order, int nl) {
+    const int l = blockIdx.x * 256 + threadIdx.x;
+    if (l < nl) order[l] = l;
+}
+
 template <int ENV>
 __global__ __launch_bounds__(256) void k_faults(const uint32_t* state, int nl, int32_t* out) {
     const int lane = blockIdx.x * 256 + threadIdx.x;
     if (lane >= nl) return;
     const LaneState<ENV>& S = *reinterpret_cast<const LaneState<ENV>*>(state + (size_t)lane * lane_words<ENV>());
     out[lane] = S.fault;
+}
+
+// Diagnostic micro-benchmark of the lane-distributed velocity sweeps (mrp_debug_velbench): a
+// synthetic v0 island of nc agent-block contacts with pcount manifold points each, swept `iters`
+// times with the early exit off; out[block] = s_memtime cycles of the sweeps.
+__global__ __launch_bounds__(BLOCK, 4) void k_velbench(int nc, int pcount, int iters, unsigned long long* out) {
+    using W = World<0>;
+    __shared__ Shared<0> sh;
+    const int tid = threadIdx.x;
+    EnvParams P{};
+    W w(sh, g_tables[0], P, tid);
+    auto& is = sh.isl;
+    if (tid == 0) {
+        is.nb = nc + 1; is.nc = nc;
+        for (int b = 0; b <= nc; ++b) { is.vvx[b] = 0.3f * b - 0.1f; is.vvy[b] = 0.2f - 0.05f * b; is.vw[b] = b == 0 ? 0.01f : 0.0f; }
+        for (int i = 0; i < nc; ++i) {
+            VC& vc = sh.u.sol.vcs[i];
+            const float ang = 0.7f * (float)i + 0.3f;
+            vc.nx = __cosf(ang); vc.ny = __sinf(ang);
+            vc.iaI = i + 1; vc.ibI = 0; vc.mA = 1.0f; vc.iA = 0.0f; vc.mB = 0.05f; vc.iB = 1.0f / 17.0833f; vc.friction = 0.44f;
+            vc.pointCount = pcount;
+            for (int j = 0; j < 2; ++j) {
+                vc.rAx[j] = 0.1f * j - 0.2f; vc.rAy[j] = 0.75f; vc.rBx[j] = 0.4f + 0.3f * j; vc.rBy[j] = -0.6f;
+                vc.ni[j] = 0.2f; vc.ti[j] = 0.01f; vc.vbias[j] = 0.0f; vc.nmass[j] = 0.9f; vc.tmass[j] = 0.8f;
+            }
+            vc.k0 = 1.2f; vc.k1 = 0.3f; vc.k3 = 1.1f; vc.nm0 = 0.9f; vc.nm1 = -0.2f; vc.nm3 = 0.95f;
+        }
+    }
+    __syncthreads();
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    int sw = nc == 1 ? w.solver_velocity_one(is, sh.u.sol.vcs, iters, false)
+                     : (nc == 2 ? w.solver_velocity_two(is, sh.u.sol.vcs, iters, false) : -1);
+    if (sw < 0) w.solver_velocity_lanes(is, sh.u.sol.vcs, iters, false);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (tid == 0) out[blockIdx.x] = t1 - t0 + (is.vvx[0] == 12345.0f ? 1ull : 0ull);
 }
 
 // ------------------------------------------------------------------------------ host side
@@ -249,6 +328,9 @@ struct mrp_ctx {
     uint32_t* d_state = nullptr;
     EnvParams params{};
     int auto_reset = 0;
+    int schedule = 0;            // dispatch lanes costliest-first (mrp_set_schedule; measured slower, off)
+    int* d_order = nullptr;      // [n_lanes] lane stepped by workgroup b
+    uint32_t* d_cost = nullptr;  // [n_lanes] last step's cycles per lane
     int have_reset = 0;
     int time_limit = 0;
     double base_puzzle = 10000.0, base_bounds = 1000.0, base_blk_bounds = 100.0;   // set_reward_params
@@ -323,6 +405,8 @@ void mrp_destroy(mrp_ctx* ctx) {
                     ctx->d_done, ctx->d_trunc, ctx->d_status, ctx->d_term, ctx->d_bodies, ctx->d_flags};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
+    if (ctx->d_order) (void)hipFree(ctx->d_order);
+    if (ctx->d_cost) (void)hipFree(ctx->d_cost);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
 }
@@ -378,6 +462,9 @@ int mrp_create(int env_id, int n_lanes, int device, uint64_t seed, uint64_t lane
     };
     for (auto& a : allocs)
         if ((e = hipMalloc(a.p, a.bytes)) != hipSuccess) return fail("hipMalloc", e);
+    if ((e = hipMalloc((void**)&ctx->d_order, nl * sizeof(int))) != hipSuccess) return fail("hipMalloc", e);
+    if ((e = hipMalloc((void**)&ctx->d_cost, nl * sizeof(uint32_t))) != hipSuccess) return fail("hipMalloc", e);
+    hipLaunchKernelGGL(k_iota, dim3((n_lanes + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_order, n_lanes);
     DISPATCH(env_id, hipLaunchKernelGGL(k_init<E>, dim3(grid_for(n_lanes)), dim3(BLOCK), 0, ctx->stream, ctx->d_state, n_lanes));
     if ((e = hipGetLastError()) != hipSuccess) return fail("k_init launch", e);
     if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return fail("k_init", e);
@@ -477,11 +564,16 @@ int mrp_step_device_ex(mrp_ctx* ctx, const float* d_actions, float* d_obs, float
     if (!ctx || !d_obs) return MRP_E_ARG;
     if (!ctx->have_reset) { ctx->err = "step() called before reset()"; return MRP_E_STATE; }
     HIPCHK(ctx, hipSetDevice(ctx->device));
+    const int sched = ctx->schedule;
     DISPATCH(ctx->env_id, hipLaunchKernelGGL(k_step<E>, dim3(grid_for(ctx->n_lanes)), dim3(BLOCK), 0, ctx->stream, ctx->d_state,
                                              ctx->n_lanes, d_actions, d_obs, d_reward, d_reward64, d_done, d_trunc, d_status,
                                              d_term, ctx->params, ctx->seed, ctx->lane_offset, ctx->auto_reset,
-                                             ctx->time_limit));
+                                             ctx->time_limit, sched ? ctx->d_order : nullptr, sched ? ctx->d_cost : nullptr));
     HIPCHK(ctx, hipGetLastError());
+    if (sched) {   // next step's dispatch order (stream-ordered behind this step)
+        hipLaunchKernelGGL(k_order, dim3(1), dim3(ORDER_NT), 0, ctx->stream, ctx->d_cost, ctx->n_lanes, ctx->d_order);
+        HIPCHK(ctx, hipGetLastError());
+    }
     return MRP_OK;
 }
 
@@ -516,6 +608,12 @@ int mrp_step_ex(mrp_ctx* ctx, const float* actions, float* obs, float* reward, d
 int mrp_step(mrp_ctx* ctx, const float* actions, float* obs, float* reward, uint8_t* done, uint8_t* trunc, uint8_t* status,
              float* term) {
     return mrp_step_ex(ctx, actions, obs, reward, nullptr, done, trunc, status, term);
+}
+
+int mrp_set_schedule(mrp_ctx* ctx, int costliest_first) {
+    if (!ctx) return MRP_E_ARG;
+    ctx->schedule = costliest_first ? 1 : 0;
+    return MRP_OK;
 }
 
 int mrp_set_seed(mrp_ctx* ctx, uint64_t seed) {
@@ -615,6 +713,20 @@ int mrp_debug_progress(int device, uint32_t** host_words, int n_lanes) {
     (void)device; (void)host_words; (void)n_lanes;
     return MRP_E_STATE;
 #endif
+}
+
+int mrp_debug_velbench(int device, int nc, int pcount, int iters, int blocks, uint64_t* cycles) {
+    if (nc < 1 || nc > 16 || pcount < 1 || pcount > 2 || blocks < 1 || !cycles || hipSetDevice(device) != hipSuccess) return MRP_E_ARG;
+    EnvTables all[5];
+    for (int i = 0; i < 5; ++i) build_tables(i, all[i]);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_tables), all, sizeof(all)) != hipSuccess) return MRP_E_HIP;
+    unsigned long long* d = nullptr;
+    if (hipMalloc((void**)&d, (size_t)blocks * 8) != hipSuccess) return MRP_E_HIP;
+    hipLaunchKernelGGL(k_velbench, dim3(blocks), dim3(BLOCK), 0, nullptr, nc, pcount, iters, d);
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(cycles, d, (size_t)blocks * 8, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    return e == hipSuccess ? MRP_OK : MRP_E_HIP;
 }
 
 int mrp_debug_stamps(int device, uint64_t* out16) {

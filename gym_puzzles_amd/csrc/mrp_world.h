@@ -29,7 +29,8 @@ constexpr int NULLN = -1;
 extern "C" __device__ int mrp_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 
 // Diagnostic phase timing (build with -DMRP_STAMPS; never in the shipped build): thread 0 of
-// every lane accumulates s_memtime deltas per phase into g_stamps.
+// every lane accumulates s_memtime deltas per phase in LDS and publishes them into g_stamps /
+// g_pmax once, at the end of its step (no global atomics inside the timed phases).
 #ifdef MRP_STAMPS
 __device__ unsigned long long g_stamps[16];     // per-phase sums over lane-steps
 __device__ unsigned long long g_pmax[16];       // per-phase max over lane-steps
@@ -41,8 +42,6 @@ __device__ uint32_t g_trace[16384][16];         // last step per lane: phases 0-
     do {                                                                                    \
         if (tid == 0) {                                                                     \
             unsigned long long _t = __builtin_amdgcn_s_memtime();                           \
-            atomicAdd(&g_stamps[k], _t - sh.stamp_t);                                       \
-            atomicMax(&g_pmax[k], _t - sh.stamp_t);                                         \
             sh.trace[k] += (uint32_t)(_t - sh.stamp_t);                                     \
             sh.stamp_t = _t;                                                                \
         }                                                                                   \
@@ -707,6 +706,9 @@ template <int ENV> struct World {
 
     // wave issue priority (s_setprio takes an immediate); `level` must be wave-uniform
     __device__ __forceinline__ static void set_prio(int level) {
+#ifdef MRP_NO_PRIO   // experiment switch: every wave at the default priority
+        return;
+#endif
         level = __builtin_amdgcn_readfirstlane(level);
         if (level >= 3) __builtin_amdgcn_s_setprio(3);
         else if (level == 2) __builtin_amdgcn_s_setprio(2);
@@ -988,7 +990,7 @@ template <int ENV> struct World {
     // once the state after sweep k equals the state after sweep k-2 bit for bit the sequence has
     // period 1 or 2 from there on and the state after sweep `iters` is the state after sweep k
     // whenever k and iters have the same parity.  The state is compared at exactly those k.
-    __device__ __forceinline__ void solver_velocity_lanes(Isl& is, VC* vcs, int iters) {
+    __device__ __forceinline__ int solver_velocity_lanes(Isl& is, VC* vcs, int iters, bool early_exit = true) {
         const int nc = is.nc;
         const VC& my = vcs[tid < nc ? tid : 0];   // lanes >= nc evaluate a copy of contact 0 and are never kept
         const float rAx0 = my.rAx[0], rAy0 = my.rAy[0], rBx0 = my.rBx[0], rBy0 = my.rBy[0];
@@ -1006,7 +1008,9 @@ template <int ENV> struct World {
         float sni0 = ni0, sni1 = ni1, sti0 = ti0, sti1 = ti1, sbx = bvx, sby = bvy, sbw = bw;
         bool have = (iters & 1) == 0;   // the initial state is sweep 0
         const int ncu = __builtin_amdgcn_readfirstlane(nc);
+        int sweeps = 0;
         for (int it = 0; it < iters; ++it) {
+            ++sweeps;
             for (int i = 0; i < ncu; ++i) {
                 // every lane evaluates ITS contact's update from contact i's body velocities;
                 // only lane i's result is kept (the Gauss-Seidel order is contact by contact)
@@ -1099,7 +1103,7 @@ template <int ENV> struct World {
                 bvx = wrl(bvx, rdl(vA.x, i), ia); bvy = wrl(bvy, rdl(vA.y, i), ia); bw = wrl(bw, rdl(wA, i), ia);
                 bvx = wrl(bvx, rdl(vB.x, i), ib); bvy = wrl(bvy, rdl(vB.y, i), ib); bw = wrl(bw, rdl(wB, i), ib);
             }
-            if (((it + 1 - iters) & 1) == 0) {   // sweep it+1 has the parity of iters
+            if (early_exit && ((it + 1 - iters) & 1) == 0) {   // sweep it+1 has the parity of iters
                 if (have) {
                     const bool same = fsame(ni0, sni0) && fsame(ni1, sni1) && fsame(ti0, sti0) && fsame(ti1, sti1) &&
                                       fsame(bvx, sbx) && fsame(bvy, sby) && fsame(bw, sbw);
@@ -1111,6 +1115,220 @@ template <int ENV> struct World {
         }
         if (tid < is.nb) { is.vvx[tid] = bvx; is.vvy[tid] = bvy; is.vw[tid] = bw; }
         if (tid < nc) { VC& o = vcs[tid]; o.ni[0] = ni0; o.ni[1] = ni1; o.ti[0] = ti0; o.ti[1] = ti1; }
+        return sweeps;
+    }
+
+    // Register-resident sweeps for islands of one or two contacts (nine in ten islands of a v0
+    // rollout have one, most of the rest two): every lane runs the same contact updates on the
+    // same values, so the bodies' velocities and the impulses stay in registers through all the
+    // sweeps - no readlane / writelane traffic - and the block solver's case tests are
+    // wave-uniform branches (ballot of identical lanes).  Same float operations in the same order
+    // as solver_velocity, same exact early exit as solver_velocity_lanes.
+    __device__ __forceinline__ static bool uni(bool c) { return __builtin_amdgcn_ballot_w64(c) != 0; }
+    struct CC {   // one contact's velocity-constraint constants (VC), in registers
+        float rAx0, rAy0, rBx0, rBy0, rAx1, rAy1, rBx1, rBy1, nmass0, nmass1, tmass0, tmass1, vbias0, vbias1;
+        float k0, k1, k3, nm0, nm1, nm3, mA, iA, mB, iB, friction;
+        V2 normal, tangent;
+        int pcount;
+        float ni0, ni1, ti0, ti1;   // impulses (state)
+    };
+    __device__ __forceinline__ static CC load_cc(const VC& c) {
+        CC o;
+        o.rAx0 = c.rAx[0]; o.rAy0 = c.rAy[0]; o.rBx0 = c.rBx[0]; o.rBy0 = c.rBy[0];
+        o.rAx1 = c.rAx[1]; o.rAy1 = c.rAy[1]; o.rBx1 = c.rBx[1]; o.rBy1 = c.rBy[1];
+        o.nmass0 = c.nmass[0]; o.nmass1 = c.nmass[1]; o.tmass0 = c.tmass[0]; o.tmass1 = c.tmass[1];
+        o.vbias0 = c.vbias[0]; o.vbias1 = c.vbias[1];
+        o.k0 = c.k0; o.k1 = c.k1; o.k3 = c.k3; o.nm0 = c.nm0; o.nm1 = c.nm1; o.nm3 = c.nm3;
+        o.mA = c.mA; o.iA = c.iA; o.mB = c.mB; o.iB = c.iB; o.friction = c.friction;
+        o.normal = v2(c.nx, c.ny); o.tangent = vcross_vs(o.normal, 1.0f);
+        o.pcount = __builtin_amdgcn_readfirstlane(c.pointCount);
+        o.ni0 = c.ni[0]; o.ni1 = c.ni[1]; o.ti0 = c.ti[0]; o.ti1 = c.ti[1];
+        return o;
+    }
+    __device__ __forceinline__ static void store_cc(VC& c, const CC& o) { c.ni[0] = o.ni0; c.ni[1] = o.ni1; c.ti[0] = o.ti0; c.ti[1] = o.ti1; }
+    // b2ContactSolver::SolveVelocityConstraints for one contact (wave-uniform values)
+    __device__ __forceinline__ static void cc_update(CC& c, V2& vA, float& wA, V2& vB, float& wB) {
+        const float mA = c.mA, iA = c.iA, mB = c.mB, iB = c.iB;
+        const V2 normal = c.normal, tangent = c.tangent;
+        {   // friction, point 0
+            V2 rA = v2(c.rAx0, c.rAy0), rB = v2(c.rBx0, c.rBy0);
+            V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
+            float vt = vdot(dv, tangent);
+            float lambda = c.tmass0 * (-vt);
+            float maxFriction = c.friction * c.ni0;
+            float newImpulse = fclamp(c.ti0 + lambda, -maxFriction, maxFriction);
+            lambda = newImpulse - c.ti0;
+            c.ti0 = newImpulse;
+            V2 P = vmul(lambda, tangent);
+            vA = vsub(vA, vmul(mA, P));
+            wA -= iA * vcross(rA, P);
+            vB = vadd(vB, vmul(mB, P));
+            wB += iB * vcross(rB, P);
+        }
+        if (c.pcount == 2) {   // friction, point 1
+            V2 rA = v2(c.rAx1, c.rAy1), rB = v2(c.rBx1, c.rBy1);
+            V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
+            float vt = vdot(dv, tangent);
+            float lambda = c.tmass1 * (-vt);
+            float maxFriction = c.friction * c.ni1;
+            float newImpulse = fclamp(c.ti1 + lambda, -maxFriction, maxFriction);
+            lambda = newImpulse - c.ti1;
+            c.ti1 = newImpulse;
+            V2 P = vmul(lambda, tangent);
+            vA = vsub(vA, vmul(mA, P));
+            wA -= iA * vcross(rA, P);
+            vB = vadd(vB, vmul(mB, P));
+            wB += iB * vcross(rB, P);
+        }
+        if (c.pcount == 1) {
+            V2 rA = v2(c.rAx0, c.rAy0), rB = v2(c.rBx0, c.rBy0);
+            V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
+            float vn = vdot(dv, normal);
+            float lambda = -c.nmass0 * (vn - c.vbias0);
+            float newImpulse = fmax_(c.ni0 + lambda, 0.0f);
+            lambda = newImpulse - c.ni0;
+            c.ni0 = newImpulse;
+            V2 P = vmul(lambda, normal);
+            vA = vsub(vA, vmul(mA, P));
+            wA -= iA * vcross(rA, P);
+            vB = vadd(vB, vmul(mB, P));
+            wB += iB * vcross(rB, P);
+        } else {
+            const float k0 = c.k0, k1 = c.k1, k2 = c.k1, k3 = c.k3, nm0 = c.nm0, nm1 = c.nm1, nm2 = c.nm1, nm3 = c.nm3;
+            V2 r1A = v2(c.rAx0, c.rAy0), r1B = v2(c.rBx0, c.rBy0);
+            V2 r2A = v2(c.rAx1, c.rAy1), r2B = v2(c.rBx1, c.rBy1);
+            V2 a = v2(c.ni0, c.ni1);
+            V2 dv1 = vsub(vsub(vadd(vB, vcross_sv(wB, r1B)), vA), vcross_sv(wA, r1A));
+            V2 dv2 = vsub(vsub(vadd(vB, vcross_sv(wB, r2B)), vA), vcross_sv(wA, r2A));
+            float vn1 = vdot(dv1, normal), vn2 = vdot(dv2, normal);
+            V2 b = v2(vn1 - c.vbias0, vn2 - c.vbias1);
+            b = vsub(b, v2(k0 * a.x + k2 * a.y, k1 * a.x + k3 * a.y));
+            V2 x = vneg(v2(nm0 * b.x + nm2 * b.y, nm1 * b.x + nm3 * b.y));
+            bool ok = true;
+            if (!uni(x.x >= 0.0f && x.y >= 0.0f)) {
+                x.x = -c.nmass0 * b.x; x.y = 0.0f;
+                vn2 = k1 * x.x + b.y;
+                if (!uni(x.x >= 0.0f && vn2 >= 0.0f)) {
+                    x.x = 0.0f; x.y = -c.nmass1 * b.y;
+                    vn1 = k2 * x.y + b.x;
+                    if (!uni(x.y >= 0.0f && vn1 >= 0.0f)) {
+                        x.x = 0.0f; x.y = 0.0f;
+                        ok = uni(b.x >= 0.0f && b.y >= 0.0f);
+                    }
+                }
+            }
+            if (ok) {
+                V2 d = vsub(x, a);
+                V2 P1 = vmul(d.x, normal), P2 = vmul(d.y, normal);
+                vA = vsub(vA, vmul(mA, vadd(P1, P2)));
+                wA -= iA * (vcross(r1A, P1) + vcross(r2A, P2));
+                vB = vadd(vB, vmul(mB, vadd(P1, P2)));
+                wB += iB * (vcross(r1B, P1) + vcross(r2B, P2));
+                c.ni0 = x.x; c.ni1 = x.y;
+            }
+        }
+    }
+    // exact early exit (see solver_velocity_lanes): compare the state after sweep k with the
+    // snapshot from sweep k-2 at the sweeps of iters' parity; true = the remaining sweeps are no-ops
+    template <int NS> struct Snap {
+        float s[NS];
+        bool have;
+        __device__ __forceinline__ bool check(const float (&cur)[NS]) {
+            bool same = have;
+#pragma unroll
+            for (int k = 0; k < NS; ++k) { same = same && fsame(cur[k], s[k]); s[k] = cur[k]; }
+            have = true;
+            return uni(same);
+        }
+    };
+    __device__ __forceinline__ int solver_velocity_one(Isl& is, VC* vcs, int iters, bool early_exit = true) {
+        CC c = load_cc(vcs[0]);
+        const int ia = vcs[0].iaI, ib = vcs[0].ibI;
+        V2 vA = v2(is.vvx[ia], is.vvy[ia]); float wA = is.vw[ia];
+        V2 vB = v2(is.vvx[ib], is.vvy[ib]); float wB = is.vw[ib];
+        Snap<10> snap = {{vA.x, vA.y, wA, vB.x, vB.y, wB, c.ni0, c.ni1, c.ti0, c.ti1}, (iters & 1) == 0};
+        int sweeps = 0;
+        for (int it = 0; it < iters; ++it) {
+            ++sweeps;
+            cc_update(c, vA, wA, vB, wB);
+            if (early_exit && ((it + 1 - iters) & 1) == 0) {
+                const float cur[10] = {vA.x, vA.y, wA, vB.x, vB.y, wB, c.ni0, c.ni1, c.ti0, c.ti1};
+                if (snap.check(cur)) break;
+            }
+        }
+        if (tid == 0) {
+            is.vvx[ia] = vA.x; is.vvy[ia] = vA.y; is.vw[ia] = wA;
+            is.vvx[ib] = vB.x; is.vvy[ib] = vB.y; is.vw[ib] = wB;
+            store_cc(vcs[0], c);
+        }
+        return sweeps;
+    }
+    // Two contacts: an island of two contacts has three bodies, X shared by both contacts, Y the
+    // other body of contact 0 and Z that of contact 1; X's role (A or B) in each contact is a
+    // template parameter, so every body access is a register.
+    template <bool XA0, bool XA1>
+    __device__ __forceinline__ int sweep_two(Isl& is, VC* vcs, int iters, bool early_exit, int x, int y, int z) {
+        CC c0 = load_cc(vcs[0]), c1 = load_cc(vcs[1]);
+        V2 vX = v2(is.vvx[x], is.vvy[x]), vY = v2(is.vvx[y], is.vvy[y]), vZ = v2(is.vvx[z], is.vvy[z]);
+        float wX = is.vw[x], wY = is.vw[y], wZ = is.vw[z];
+        Snap<17> snap = {{vX.x, vX.y, wX, vY.x, vY.y, wY, vZ.x, vZ.y, wZ, c0.ni0, c0.ni1, c0.ti0, c0.ti1,
+                          c1.ni0, c1.ni1, c1.ti0, c1.ti1}, (iters & 1) == 0};
+        int sweeps = 0;
+        for (int it = 0; it < iters; ++it) {
+            ++sweeps;
+            if (XA0) cc_update(c0, vX, wX, vY, wY); else cc_update(c0, vY, wY, vX, wX);
+            if (XA1) cc_update(c1, vX, wX, vZ, wZ); else cc_update(c1, vZ, wZ, vX, wX);
+            if (early_exit && ((it + 1 - iters) & 1) == 0) {
+                const float cur[17] = {vX.x, vX.y, wX, vY.x, vY.y, wY, vZ.x, vZ.y, wZ, c0.ni0, c0.ni1, c0.ti0, c0.ti1,
+                                       c1.ni0, c1.ni1, c1.ti0, c1.ti1};
+                if (snap.check(cur)) break;
+            }
+        }
+        if (tid == 0) {   // contact 1 stores last, as the reference's per-contact write-back order leaves it
+            is.vvx[x] = vX.x; is.vvy[x] = vX.y; is.vw[x] = wX;
+            is.vvx[y] = vY.x; is.vvy[y] = vY.y; is.vw[y] = wY;
+            is.vvx[z] = vZ.x; is.vvy[z] = vZ.y; is.vw[z] = wZ;
+            store_cc(vcs[0], c0); store_cc(vcs[1], c1);
+        }
+        return sweeps;
+    }
+    // Two contacts between the same two bodies (e.g. an agent against both boxes of the T block):
+    // contact 1 is (P, Q) when SAME, else (Q, P).
+    template <bool SAME>
+    __device__ __forceinline__ int sweep_same(Isl& is, VC* vcs, int iters, bool early_exit, int p, int q) {
+        CC c0 = load_cc(vcs[0]), c1 = load_cc(vcs[1]);
+        V2 vP = v2(is.vvx[p], is.vvy[p]), vQ = v2(is.vvx[q], is.vvy[q]);
+        float wP = is.vw[p], wQ = is.vw[q];
+        Snap<14> snap = {{vP.x, vP.y, wP, vQ.x, vQ.y, wQ, c0.ni0, c0.ni1, c0.ti0, c0.ti1, c1.ni0, c1.ni1, c1.ti0, c1.ti1},
+                         (iters & 1) == 0};
+        int sweeps = 0;
+        for (int it = 0; it < iters; ++it) {
+            ++sweeps;
+            cc_update(c0, vP, wP, vQ, wQ);
+            if (SAME) cc_update(c1, vP, wP, vQ, wQ); else cc_update(c1, vQ, wQ, vP, wP);
+            if (early_exit && ((it + 1 - iters) & 1) == 0) {
+                const float cur[14] = {vP.x, vP.y, wP, vQ.x, vQ.y, wQ, c0.ni0, c0.ni1, c0.ti0, c0.ti1, c1.ni0, c1.ni1, c1.ti0, c1.ti1};
+                if (snap.check(cur)) break;
+            }
+        }
+        if (tid == 0) {
+            is.vvx[p] = vP.x; is.vvy[p] = vP.y; is.vw[p] = wP;
+            is.vvx[q] = vQ.x; is.vvy[q] = vQ.y; is.vw[q] = wQ;
+            store_cc(vcs[0], c0); store_cc(vcs[1], c1);
+        }
+        return sweeps;
+    }
+    // returns -1 when the two contacts share no body (cannot happen inside one island; the caller
+    // then uses solver_velocity_lanes)
+    __device__ __forceinline__ int solver_velocity_two(Isl& is, VC* vcs, int iters, bool early_exit = true) {
+        const int a0 = vcs[0].iaI, b0 = vcs[0].ibI, a1 = vcs[1].iaI, b1 = vcs[1].ibI;
+        if (a0 == a1 && b0 == b1) return sweep_same<true>(is, vcs, iters, early_exit, a0, b0);
+        if (a0 == b1 && b0 == a1) return sweep_same<false>(is, vcs, iters, early_exit, a0, b0);
+        if (a0 == a1) return sweep_two<true, true>(is, vcs, iters, early_exit, a0, b0, b1);
+        if (a0 == b1) return sweep_two<true, false>(is, vcs, iters, early_exit, a0, b0, a1);
+        if (b0 == a1) return sweep_two<false, true>(is, vcs, iters, early_exit, b0, a0, b1);
+        if (b0 == b1) return sweep_two<false, false>(is, vcs, iters, early_exit, b0, a0, a1);
+        return -1;
     }
 
     // ---------------------------------------------------------------- lane-distributed position iterations
@@ -1253,7 +1471,6 @@ template <int ENV> struct World {
         }
         MRP_TRACE(12, is.nc);
         if (is.nc > 0) {
-            MRP_TRACE(15, 1);
             solver_init(is, vcs, pcs, true, dtRatio);
             solver_init_velocity(is, vcs, pcs);
             solver_warm_start(is, vcs);
@@ -1340,7 +1557,10 @@ template <int ENV> struct World {
             const int lvl = nc >= 6 ? 3 : (nc >= 4 ? 2 : (nc >= 2 ? 1 : 0));
             if (nc > 0 && nc <= 64) {
                 set_prio(lvl > step_prio ? lvl : step_prio);
-                solver_velocity_lanes(is, sh.u.sol.vcs, 180);
+                int sweeps = nc == 1 ? solver_velocity_one(is, sh.u.sol.vcs, 180) : (nc == 2 ? solver_velocity_two(is, sh.u.sol.vcs, 180) : -1);
+                if (sweeps < 0) sweeps = solver_velocity_lanes(is, sh.u.sol.vcs, 180);
+                MRP_TRACE(15, sweeps * nc);
+                (void)sweeps;
             }
             else if (nc > 64 && tid == 0) for (int it = 0; it < 180; ++it) solver_velocity(is, sh.u.sol.vcs);
             __syncthreads();
@@ -1796,7 +2016,9 @@ template <int ENV> struct World {
                 if (tid == 0) island_toi_mid(sh.isl, sh.u.sol.vcs, sh.u.sol.pcs);
                 __syncthreads();
                 if (nc <= 64) {
-                    solver_velocity_lanes(sh.isl, sh.u.sol.vcs, 180);
+                    int sweeps = nc == 1 ? solver_velocity_one(sh.isl, sh.u.sol.vcs, 180)
+                                         : (nc == 2 ? solver_velocity_two(sh.isl, sh.u.sol.vcs, 180) : -1);
+                    if (sweeps < 0) solver_velocity_lanes(sh.isl, sh.u.sol.vcs, 180);
                     set_prio(step_prio);
                 }
                 else if (tid == 0) for (int i = 0; i < 180; ++i) solver_velocity(sh.isl, sh.u.sol.vcs);

@@ -111,6 +111,10 @@ int mrp_set_auto_reset(mrp_ctx* ctx, int enabled);
  * lanes, parameters, stream or time limit: SB3 VecEnv.seed(seed) (train/train.py:63-75 seeds
  * every env before the first reset).  Per-lane streams stay keyed by the global lane index. */
 int mrp_set_seed(mrp_ctx* ctx, uint64_t seed);
+/* Lane scheduling (default off): each step dispatches the lanes in descending order of their
+ * previous step's cost, so the long serial solver chains start first (one small sort kernel per
+ * step).  Results never depend on it.  Measured 1-2 % slower on v0 at 4096 lanes. */
+int mrp_set_schedule(mrp_ctx* ctx, int costliest_first);
 /* TimeLimit max_episode_steps applied inside mrp_step (default: the registered value of
  * gym_puzzles/__init__.py:6-27); 0 disables it (when an outer gym.wrappers.TimeLimit is used). */
 int mrp_set_time_limit(mrp_ctx* ctx, int max_episode_steps);
@@ -164,6 +168,10 @@ int mrp_debug_trace(int device, uint32_t* out, int n_lanes);
  * thread 0 overwrites with the last progress point it reached; readable while a launch runs
  * (hang localisation).  Returns MRP_E_STATE in the shipped build. */
 int mrp_debug_progress(int device, uint32_t** host_words, int n_lanes);
+/* Diagnostic micro-benchmark: `blocks` workgroups each sweep a synthetic v0 island (nc agent-block
+ * contacts of pcount points) `iters` times with the early exit off; cycles[block] = s_memtime
+ * cycles of the sweeps (per-contact-update cost = cycles / (iters * nc)). */
+int mrp_debug_velbench(int device, int nc, int pcount, int iters, int blocks, uint64_t* cycles);
 
 /* ------------------------------------------------------------------------------------------
  * On-device VecNormalize + Monitor statistics.  Replaces the host-side

@@ -255,3 +255,26 @@ def test_step_device_with_torch_stream(gpu_lib):
     _eq("obs", obs.cpu().numpy(), h.obs)
     _eq("reward", rew.cpu().numpy(), h.reward)
     _eq("done", done.cpu().numpy(), h.done)
+
+
+def test_costliest_first_schedule_changes_nothing(gpu_lib):
+    """Lane scheduling (mrp_set_schedule) only permutes which workgroup steps which lane: every
+    output and the full lane state must be bit-identical to lane-order dispatch."""
+    from gym_puzzles_amd import Batch
+    lanes, steps = 512, 60
+    a, b = Batch(0, lanes, seed=5), Batch(0, lanes, seed=5)
+    a.set_schedule(True)
+    b.set_schedule(False)
+    for x in (a, b):
+        x.set_auto_reset(True)
+        x.set_time_limit(25)
+    _eq("reset", a.reset(), b.reset())
+    for t in range(steps):
+        oa, ra, da, _ = a.step()
+        ob, rb, db, _ = b.step()
+        _eq(f"obs@{t}", oa, ob)
+        _eq(f"reward@{t}", ra, rb)
+        _eq(f"done@{t}", da, db)
+    _eq("state", a.get_state(), b.get_state())
+    a.close()
+    b.close()

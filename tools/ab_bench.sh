@@ -1,0 +1,15 @@
+#!/bin/bash
+# A/B of library builds on the GPU box: tools/ab_bench.sh libA.so libB.so ...  (bench 20/5 and 200/20, twice each, interleaved)
+set -uo pipefail
+mkdir -p gpurun_out
+out=gpurun_out/ab.txt; : > $out
+libs=("$@")
+for rep in 1 2; do
+  for lib in "${libs[@]}"; do
+    for cfg in "20 5" "200 20"; do
+      read -r K W <<< "$cfg"
+      r=$(MRP_LIB=$lib timeout -k 5 120 python bench.py --steps $K --warmup $W --no-cpu-baseline --later-window 0 2>/dev/null | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('%.3fM' % (d['value']/1e6), 'kernel %.3f ms' % d['roofline']['kernel_ms'])") || { echo "bench failed for $lib"; exit 1; }
+      echo "$lib steps=$K warmup=$W: $r" | tee -a $out
+    done
+  done
+done
