@@ -75,7 +75,7 @@ def main():
     ap.add_argument("--seed", type=int, default=17)
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the per-step gather to rank 0")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--schedule", action="store_true", help="dispatch lanes costliest-first (mrp_set_schedule)")
+    ap.add_argument("--schedule", type=int, default=0, help="mrp_set_schedule mode: 1 costliest-first dispatch, 2 cost priority, 3 both")
     ap.add_argument("--later-window", type=int, default=200,
                     help="diagnostic: also time this many steps starting near --later-start (0 = off; N=1 only)")
     ap.add_argument("--later-start", type=int, default=500)

@@ -216,9 +216,10 @@ class Batch:
         self._check(load().mrp_step_device_ex(self._h, d_actions, d_obs, d_reward, d_reward64, d_done, d_trunc, d_status,
                                               d_term))
 
-    def set_schedule(self, costliest_first: bool):
-        """Dispatch lanes costliest-first (default) or in lane order; results are identical."""
-        self._check(load().mrp_set_schedule(self._h, 1 if costliest_first else 0))
+    def set_schedule(self, mode):
+        """Lane scheduling (mrp_set_schedule): 0 off, 1 costliest-first dispatch, 2 issue priority
+        from the previous step's cost, 3 both (True = 1); results are identical in every mode."""
+        self._check(load().mrp_set_schedule(self._h, int(mode)))
 
     def set_seed(self, seed: int):
         """Re-key the device RNG (later resets and synthetic actions); lanes, parameters, stream

@@ -133,7 +133,8 @@ template <int ENV>
 __global__ __launch_bounds__(BLOCK, 4) void k_step(uint32_t* state, int nl, const float* actions, float* obs, float* reward,
                                                 double* reward64, uint8_t* done_out, uint8_t* trunc_out, uint8_t* status_out, float* term_obs,
                                                 EnvParams P, uint64_t seed, uint64_t lane_offset, int auto_reset,
-                                                int max_steps, const int* __restrict__ order, uint32_t* __restrict__ cost) {
+                                                int max_steps, const int* __restrict__ order, uint32_t* __restrict__ cost,
+                                                const uint32_t* __restrict__ costmax) {
     using D = Dims<ENV>;
     __shared__ Shared<ENV> sh;
     __shared__ int s_fin;
@@ -163,6 +164,11 @@ __global__ __launch_bounds__(BLOCK, 4) void k_step(uint32_t* state, int nl, cons
     __syncthreads();
     if (tid == 0) sh.S.stepCounter += 1;
     Env<ENV> e(sh, g_tables[ENV], P, tid);
+    if (costmax) {   // priority from the lane's previous-step cost relative to the slowest lane's
+        const uint64_t c = cost[lane], m = *costmax;
+        e.prio_floor = __builtin_amdgcn_readfirstlane(4 * c > 3 * m ? 3 : (2 * c > m ? 2 : (4 * c > m ? 1 : 0)));
+        e.set_prio(e.prio_floor);
+    }
     e.env_step_coop();
     if (tid == 0) {
         sh.S.elapsed += 1;
@@ -236,7 +242,8 @@ __global__ __launch_bounds__(BLOCK) void k_bodies(const uint32_t* state, int nl,
 // Dispatch order for the next step: lanes by descending cost of this step (counting sort over 64
 // linear buckets of [0, max cost]; order inside a bucket is arbitrary and never affects results).
 constexpr int ORDER_NT = 1024, ORDER_NB = 64;
-__global__ __launch_bounds__(ORDER_NT) void k_order(const uint32_t* __restrict__ cost, int nl, int* __restrict__ order) {
+__global__ __launch_bounds__(ORDER_NT) void k_order(const uint32_t* __restrict__ cost, int nl, int* __restrict__ order,
+                                                    uint32_t* __restrict__ costmax) {
     __shared__ uint32_t s_max;
     __shared__ int s_cnt[ORDER_NB], s_base[ORDER_NB];
     const int t = threadIdx.x;
@@ -248,6 +255,8 @@ __global__ __launch_bounds__(ORDER_NT) void k_order(const uint32_t* __restrict__
     atomicMax(&s_max, m);
     __syncthreads();
     const uint64_t mx = s_max;
+    if (t == 0 && costmax) *costmax = s_max;
+    if (!order) return;
     for (int l = t; l < nl; l += ORDER_NT) {
         const int b = (ORDER_NB - 1) - (int)(((uint64_t)cost[l] * (ORDER_NB - 1)) / mx);   // bucket 0 = costliest
         atomicAdd(&s_cnt[b], 1);
@@ -331,6 +340,7 @@ struct mrp_ctx {
     int schedule = 0;            // dispatch lanes costliest-first (mrp_set_schedule; measured slower, off)
     int* d_order = nullptr;      // [n_lanes] lane stepped by workgroup b
     uint32_t* d_cost = nullptr;  // [n_lanes] last step's cycles per lane
+    uint32_t* d_costmax = nullptr;   // max of d_cost (priority mode)
     int have_reset = 0;
     int time_limit = 0;
     double base_puzzle = 10000.0, base_bounds = 1000.0, base_blk_bounds = 100.0;   // set_reward_params
@@ -407,6 +417,7 @@ void mrp_destroy(mrp_ctx* ctx) {
         if (p) (void)hipFree(p);
     if (ctx->d_order) (void)hipFree(ctx->d_order);
     if (ctx->d_cost) (void)hipFree(ctx->d_cost);
+    if (ctx->d_costmax) (void)hipFree(ctx->d_costmax);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
 }
@@ -464,6 +475,9 @@ int mrp_create(int env_id, int n_lanes, int device, uint64_t seed, uint64_t lane
         if ((e = hipMalloc(a.p, a.bytes)) != hipSuccess) return fail("hipMalloc", e);
     if ((e = hipMalloc((void**)&ctx->d_order, nl * sizeof(int))) != hipSuccess) return fail("hipMalloc", e);
     if ((e = hipMalloc((void**)&ctx->d_cost, nl * sizeof(uint32_t))) != hipSuccess) return fail("hipMalloc", e);
+    if ((e = hipMalloc((void**)&ctx->d_costmax, sizeof(uint32_t))) != hipSuccess) return fail("hipMalloc", e);
+    if ((e = hipMemset(ctx->d_cost, 0, nl * sizeof(uint32_t))) != hipSuccess) return fail("hipMemset", e);
+    if ((e = hipMemset(ctx->d_costmax, 0xff, sizeof(uint32_t))) != hipSuccess) return fail("hipMemset", e);
     hipLaunchKernelGGL(k_iota, dim3((n_lanes + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_order, n_lanes);
     DISPATCH(env_id, hipLaunchKernelGGL(k_init<E>, dim3(grid_for(n_lanes)), dim3(BLOCK), 0, ctx->stream, ctx->d_state, n_lanes));
     if ((e = hipGetLastError()) != hipSuccess) return fail("k_init launch", e);
@@ -568,10 +582,12 @@ int mrp_step_device_ex(mrp_ctx* ctx, const float* d_actions, float* d_obs, float
     DISPATCH(ctx->env_id, hipLaunchKernelGGL(k_step<E>, dim3(grid_for(ctx->n_lanes)), dim3(BLOCK), 0, ctx->stream, ctx->d_state,
                                              ctx->n_lanes, d_actions, d_obs, d_reward, d_reward64, d_done, d_trunc, d_status,
                                              d_term, ctx->params, ctx->seed, ctx->lane_offset, ctx->auto_reset,
-                                             ctx->time_limit, sched ? ctx->d_order : nullptr, sched ? ctx->d_cost : nullptr));
+                                             ctx->time_limit, (sched & 1) ? ctx->d_order : nullptr, sched ? ctx->d_cost : nullptr,
+                                             (sched & 2) ? ctx->d_costmax : nullptr));
     HIPCHK(ctx, hipGetLastError());
-    if (sched) {   // next step's dispatch order (stream-ordered behind this step)
-        hipLaunchKernelGGL(k_order, dim3(1), dim3(ORDER_NT), 0, ctx->stream, ctx->d_cost, ctx->n_lanes, ctx->d_order);
+    if (sched) {   // next step's dispatch order / cost scale (stream-ordered behind this step)
+        hipLaunchKernelGGL(k_order, dim3(1), dim3(ORDER_NT), 0, ctx->stream, ctx->d_cost, ctx->n_lanes,
+                           (sched & 1) ? ctx->d_order : nullptr, ctx->d_costmax);
         HIPCHK(ctx, hipGetLastError());
     }
     return MRP_OK;
@@ -612,7 +628,8 @@ int mrp_step(mrp_ctx* ctx, const float* actions, float* obs, float* reward, uint
 
 int mrp_set_schedule(mrp_ctx* ctx, int costliest_first) {
     if (!ctx) return MRP_E_ARG;
-    ctx->schedule = costliest_first ? 1 : 0;
+    if (costliest_first < 0 || costliest_first > 3) return MRP_E_ARG;
+    ctx->schedule = costliest_first;
     return MRP_OK;
 }
 

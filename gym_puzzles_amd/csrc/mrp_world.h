@@ -245,6 +245,7 @@ template <int ENV> struct World {
     const EnvParams& P;
     const int tid;
     int step_prio = 0;   // issue priority of this lane for the rest of the step (wave-uniform)
+    int prio_floor = 0;  // lower bound for step_prio (k_step: from the lane's previous-step cost)
 
     __device__ __forceinline__ World(SH& s, const EnvTables& t, const EnvParams& p, int thread) : sh(s), S(s.S), L(s.lt), T(t), P(p), tid(thread) {}
 
@@ -692,6 +693,7 @@ template <int ENV> struct World {
         }
         touching = __builtin_amdgcn_readfirstlane(touching);
         step_prio = touching >= 4 ? 2 : (touching >= 2 ? 1 : 0);
+        if (prio_floor > step_prio) step_prio = prio_floor;
         set_prio(step_prio);
         __syncthreads();
         if (tid == 0) {
@@ -986,6 +988,8 @@ template <int ENV> struct World {
     // lane l of `old` replaced by the wave-uniform x (v_writelane_b32)
     __device__ __forceinline__ static float wrl(float old, float x, int l) { return __int_as_float(mrp_writelane(__float_as_int(x), l, __float_as_int(old))); }
     __device__ __forceinline__ static bool fsame(float a, float b) { return __float_as_uint(a) == __float_as_uint(b); }
+    // lane l's value of a per-lane condition, wave-uniform (ballot + bit test: no readlane)
+    __device__ __forceinline__ static bool lane_bit(bool c, int l) { return (__builtin_amdgcn_ballot_w64(c) >> l) & 1ull; }
     // Early exit, exact: one sweep is a pure function of (body velocities, contact impulses), so
     // once the state after sweep k equals the state after sweep k-2 bit for bit the sequence has
     // period 1 or 2 from there on and the state after sweep `iters` is the state after sweep k
@@ -1077,15 +1081,15 @@ template <int ENV> struct World {
                     // branches); the other lanes follow lane i's case and are discarded
                     V2 x = vneg(v2(nm0 * b.x + nm2 * b.y, nm1 * b.x + nm3 * b.y));
                     bool ok = true;
-                    if (!(rdl(x.x, i) >= 0.0f && rdl(x.y, i) >= 0.0f)) {
+                    if (!lane_bit(x.x >= 0.0f && x.y >= 0.0f, i)) {
                         x.x = -nmass0 * b.x; x.y = 0.0f;
                         vn2 = k1 * x.x + b.y;
-                        if (!(rdl(x.x, i) >= 0.0f && rdl(vn2, i) >= 0.0f)) {
+                        if (!lane_bit(x.x >= 0.0f && vn2 >= 0.0f, i)) {
                             x.x = 0.0f; x.y = -nmass1 * b.y;
                             vn1 = k2 * x.y + b.x;
-                            if (!(rdl(x.y, i) >= 0.0f && rdl(vn1, i) >= 0.0f)) {
+                            if (!lane_bit(x.y >= 0.0f && vn1 >= 0.0f, i)) {
                                 x.x = 0.0f; x.y = 0.0f;
-                                ok = rdl(b.x, i) >= 0.0f && rdl(b.y, i) >= 0.0f;
+                                ok = lane_bit(b.x >= 0.0f && b.y >= 0.0f, i);
                             }
                         }
                     }
@@ -1354,6 +1358,131 @@ template <int ENV> struct World {
             return q;
         }
     };
+    // Register-resident position passes for islands of one or two contacts (the topologies of
+    // solver_velocity_one / _two): every lane runs the same point updates on the same values, so
+    // the bodies' positions stay in registers, the rotation memo is wave-uniform and nothing goes
+    // through readlane / writelane.  Same float operations in the same order as solver_position.
+    struct UniMemo {   // RotMemo with wave-uniform (identical-lane) angles: scalar branches
+        uint32_t k0 = 0u, k1 = 0u;
+        Rot q0 = {0.0f, 1.0f}, q1 = {0.0f, 1.0f};
+        bool next1 = false;
+        __device__ __forceinline__ Rot get(float angle) {
+            const uint32_t b = __float_as_uint(angle);
+            if (uni(b == k0)) return q0;
+            if (uni(b == k1)) return q1;
+            const Rot q = rot(angle);
+            if (next1) { k1 = b; q1 = q; } else { k0 = b; q0 = q; }
+            next1 = !next1;
+            return q;
+        }
+    };
+    struct PCC {   // one contact's position-constraint constants (PC + masses), in registers
+        float lcAx, lcAy, lcBx, lcBy, lnx, lny, lpx0, lpy0, qx0, qy0, qx1, qy1, radA, radB, mA, iA, mB, iB;
+        int pcount, type;
+    };
+    __device__ __forceinline__ static PCC load_pcc(const VC& vc, const PC& pc, bool toi, int toiA, int toiB) {
+        PCC o;
+        o.lcAx = pc.lcAx; o.lcAy = pc.lcAy; o.lcBx = pc.lcBx; o.lcBy = pc.lcBy;
+        o.lnx = pc.lnx; o.lny = pc.lny; o.lpx0 = pc.lpx0; o.lpy0 = pc.lpy0;
+        o.qx0 = pc.lpx[0]; o.qy0 = pc.lpy[0]; o.qx1 = pc.lpx[1]; o.qy1 = pc.lpy[1];
+        o.radA = pc.rA; o.radB = pc.rB;
+        o.mA = vc.mA; o.iA = vc.iA; o.mB = vc.mB; o.iB = vc.iB;
+        if (toi) {
+            if (!(vc.iaI == toiA || vc.iaI == toiB)) { o.mA = 0.0f; o.iA = 0.0f; }
+            if (!(vc.ibI == toiA || vc.ibI == toiB)) { o.mB = 0.0f; o.iB = 0.0f; }
+        }
+        o.pcount = __builtin_amdgcn_readfirstlane(pc.pointCount);
+        o.type = __builtin_amdgcn_readfirstlane(pc.type);
+        return o;
+    }
+    // b2ContactSolver::SolvePositionConstraints for one contact (wave-uniform values)
+    __device__ __forceinline__ static void pcc_update(const PCC& c, V2& cA, float& aA, V2& cB, float& aB, float& minSep,
+                                                      float baum, UniMemo& memo) {
+        for (int j = 0; j < 2; ++j) {
+            if (j == c.pcount) break;
+            Xf xA, xB;
+            xA.q = memo.get(aA); xB.q = memo.get(aB);
+            xA.p = vsub(cA, mul_rv(xA.q, v2(c.lcAx, c.lcAy)));
+            xB.p = vsub(cB, mul_rv(xB.q, v2(c.lcBx, c.lcBy)));
+            const V2 lp = j == 0 ? v2(c.qx0, c.qy0) : v2(c.qx1, c.qy1);
+            V2 normal, point; float sep;
+            if (c.type == MT_FACEA) {
+                normal = mul_rv(xA.q, v2(c.lnx, c.lny));
+                V2 planePoint = mul_xv(xA, v2(c.lpx0, c.lpy0));
+                V2 clipPoint = mul_xv(xB, lp);
+                sep = vdot(vsub(clipPoint, planePoint), normal) - c.radA - c.radB;
+                point = clipPoint;
+            } else {
+                normal = mul_rv(xB.q, v2(c.lnx, c.lny));
+                V2 planePoint = mul_xv(xB, v2(c.lpx0, c.lpy0));
+                V2 clipPoint = mul_xv(xA, lp);
+                sep = vdot(vsub(clipPoint, planePoint), normal) - c.radA - c.radB;
+                point = clipPoint;
+                normal = vneg(normal);
+            }
+            V2 rA = vsub(point, cA), rB = vsub(point, cB);
+            minSep = fmin_(minSep, sep);
+            float Cc = fclamp(baum * (sep + LINEAR_SLOP), -MAX_LINEAR_CORRECTION, 0.0f);
+            float rnA = vcross(rA, normal), rnB = vcross(rB, normal);
+            float K = c.mA + c.mB + c.iA * rnA * rnA + c.iB * rnB * rnB;
+            float impulse = K > 0.0f ? -Cc / K : 0.0f;
+            V2 Pv = vmul(impulse, normal);
+            cA = vsub(cA, vmul(c.mA, Pv));
+            aA -= c.iA * vcross(rA, Pv);
+            cB = vadd(cB, vmul(c.mB, Pv));
+            aB += c.iB * vcross(rB, Pv);
+        }
+    }
+    // NC = 1: contact 0 on (P, Q).  NC = 2: SAMEB - both contacts on P, Q (contact 1 as (P, Q) if
+    // XA1 else (Q, P)); otherwise X (= P) shared, Y (= Q) the other body of contact 0, Z of contact 1,
+    // X's role in contact k given by XA0 / XA1.
+    template <int NC, bool SAMEB, bool XA0, bool XA1>
+    __device__ __forceinline__ int pos_sweep(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB, int iters,
+                                             int p, int q, int z) {
+        const PCC c0 = load_pcc(vcs[0], pcs[0], toi, toiA, toiB);
+        const PCC c1 = load_pcc(vcs[NC - 1], pcs[NC - 1], toi, toiA, toiB);
+        V2 cP = v2(is.pcx[p], is.pcy[p]), cQ = v2(is.pcx[q], is.pcy[q]), cZ = v2(is.pcx[z], is.pcy[z]);
+        float aP = is.pa[p], aQ = is.pa[q], aZ = is.pa[z];
+        const float baum = toi ? TOI_BAUMGARTE : BAUMGARTE;
+        const float exitSep = toi ? -1.5f * LINEAR_SLOP : -3.0f * LINEAR_SLOP;
+        UniMemo memo;
+        int it = 0;
+        while (it < iters) {
+            ++it;
+            float minSep = 0.0f;
+            if (NC == 1 || SAMEB) {
+                if (XA0) pcc_update(c0, cP, aP, cQ, aQ, minSep, baum, memo); else pcc_update(c0, cQ, aQ, cP, aP, minSep, baum, memo);
+                if (NC == 2) { if (XA1) pcc_update(c1, cP, aP, cQ, aQ, minSep, baum, memo); else pcc_update(c1, cQ, aQ, cP, aP, minSep, baum, memo); }
+            } else {
+                if (XA0) pcc_update(c0, cP, aP, cQ, aQ, minSep, baum, memo); else pcc_update(c0, cQ, aQ, cP, aP, minSep, baum, memo);
+                if (XA1) pcc_update(c1, cP, aP, cZ, aZ, minSep, baum, memo); else pcc_update(c1, cZ, aZ, cP, aP, minSep, baum, memo);
+            }
+            if (uni(minSep >= exitSep)) break;
+        }
+        if (tid == 0) {
+            is.pcx[p] = cP.x; is.pcy[p] = cP.y; is.pa[p] = aP;
+            is.pcx[q] = cQ.x; is.pcy[q] = cQ.y; is.pa[q] = aQ;
+            if (NC == 2 && !SAMEB) { is.pcx[z] = cZ.x; is.pcy[z] = cZ.y; is.pa[z] = aZ; }
+        }
+        return it;
+    }
+    // position passes of a one- or two-contact island; -1 = other topology (use the lanes version)
+    __device__ __forceinline__ int solver_position_small(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB,
+                                                         int iters) {
+        const int nc = __builtin_amdgcn_readfirstlane(is.nc);
+        const int a0 = vcs[0].iaI, b0 = vcs[0].ibI;
+        if (nc == 1) return pos_sweep<1, true, true, true>(is, vcs, pcs, toi, toiA, toiB, iters, a0, b0, b0);
+        if (nc != 2) return -1;
+        const int a1 = vcs[1].iaI, b1 = vcs[1].ibI;
+        if (a0 == a1 && b0 == b1) return pos_sweep<2, true, true, true>(is, vcs, pcs, toi, toiA, toiB, iters, a0, b0, b0);
+        if (a0 == b1 && b0 == a1) return pos_sweep<2, true, true, false>(is, vcs, pcs, toi, toiA, toiB, iters, a0, b0, b0);
+        if (a0 == a1) return pos_sweep<2, false, true, true>(is, vcs, pcs, toi, toiA, toiB, iters, a0, b0, b1);
+        if (a0 == b1) return pos_sweep<2, false, true, false>(is, vcs, pcs, toi, toiA, toiB, iters, a0, b0, a1);
+        if (b0 == a1) return pos_sweep<2, false, false, true>(is, vcs, pcs, toi, toiA, toiB, iters, b0, a0, b1);
+        if (b0 == b1) return pos_sweep<2, false, false, false>(is, vcs, pcs, toi, toiA, toiB, iters, b0, a0, a1);
+        return -1;
+    }
+
     __device__ __forceinline__ int solver_position_lanes(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB, int iters) {
         const int nc = is.nc;
         const int me = tid < nc ? tid : 0;   // lanes >= nc evaluate a copy of contact 0 and are never kept
@@ -1485,7 +1614,8 @@ template <int ENV> struct World {
     // the reference's loop does
     __device__ __forceinline__ void island_position(Isl& is, VC* vcs, PC* pcs, int nc) {
         if (nc > 0 && nc <= 64) {
-            const int n = solver_position_lanes(is, vcs, pcs, false, -1, -1, 60);
+            int n = solver_position_small(is, vcs, pcs, false, -1, -1, 60);
+            if (n < 0) n = solver_position_lanes(is, vcs, pcs, false, -1, -1, 60);
             if (tid == 0) S.posIters += n;
         } else if (tid == 0) {
             if (nc > 0) {
@@ -2008,7 +2138,8 @@ template <int ENV> struct World {
                 const int nc = __builtin_amdgcn_readfirstlane(sh.isl.nc);
                 if (nc <= 64) {
                     set_prio(2 > step_prio ? 2 : step_prio);   // a TOI event is on this lane's critical path
-                    solver_position_lanes(sh.isl, sh.u.sol.vcs, sh.u.sol.pcs, true, sh.toiIA, sh.toiIB, 20);
+                    if (solver_position_small(sh.isl, sh.u.sol.vcs, sh.u.sol.pcs, true, sh.toiIA, sh.toiIB, 20) < 0)
+                        solver_position_lanes(sh.isl, sh.u.sol.vcs, sh.u.sol.pcs, true, sh.toiIA, sh.toiIB, 20);
                 } else if (tid == 0) {
                     for (int i = 0; i < 20; ++i) if (solver_position(sh.isl, sh.u.sol.vcs, sh.u.sol.pcs, true, sh.toiIA, sh.toiIB)) break;
                 }
