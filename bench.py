@@ -27,10 +27,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 ENV_NAMES = {0: "MultiRobotPuzzle-v0", 1: "MultiRobotPuzzleHeavy-v0", 2: "MultiRobotPuzzle-v2",
-             3: "MultiRobotPuzzleHeavy-v2", 4: "MultiRobotPuzzleHeavy-v2-3block"}
+             3: "MultiRobotPuzzleHeavy-v2", 4: "MultiRobotPuzzleHeavy-v2-3block", 5: "MultiRobotPuzzle-v3",
+             6: "MultiRobotPuzzle-v3-heavy"}
 # Algorithmic HBM bytes per env-step: mutable per-lane state read+written
 # once per step plus I/O; shared geometry/mass tables excluded.
-ALGO_BYTES = {0: 1657, 1: 3547, 2: 3613, 3: 3613, 4: 6085}
+ALGO_BYTES = {0: 1657, 1: 3547, 2: 3613, 3: 3613, 4: 6085, 5: 1653, 6: 1653}   # v3: v0's lane state, 27-float obs
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 
 

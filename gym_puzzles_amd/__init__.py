@@ -14,7 +14,7 @@ from ._native import ENV_IDS, Batch, MrpError, env_dims  # noqa: F401
 def __getattr__(name):
     # the env classes import lazily so that `import gym_puzzles_amd` never touches the GPU
     if name in ("MultiRobotPuzzle", "MultiRobotPuzzleHeavy", "MultiRobotPuzzle2", "MultiRobotPuzzleHeavy2",
-                "MultiRobotPuzzleHeavy2ThreeBlock", "make"):
+                "MultiRobotPuzzleHeavy2ThreeBlock", "RobotPuzzleBase", "make"):
         from . import envs
         return getattr(envs, name)
     if name in ("MultiRobotPuzzleVecEnv", "MultiRobotPuzzleVecNormalize", "DeviceVecNormalize"):

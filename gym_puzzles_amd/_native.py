@@ -23,6 +23,8 @@ ENV_IDS = {
     "MultiRobotPuzzle-v2": 2,
     "MultiRobotPuzzleHeavy-v2": 3,
     "MultiRobotPuzzleHeavy-v2-3block": 4,
+    "MultiRobotPuzzle-v3": 5,
+    "MultiRobotPuzzle-v3-heavy": 6,      # RobotPuzzleBase(heavy=True) (tests/test_env.py:12)
 }
 
 # every symbol include/mrp.h declares (tests/test_abi.py checks the .so exports all of them)
@@ -177,8 +179,10 @@ class Batch:
         return self._h
 
     def set_reward_params(self, agentDelta=None, agentDistance=None, blockDelta=None, blockDistance=None,
-                          puzzleComp=10000, outOfBounds=1000, blkOutOfBounds=100):
-        v0 = self.env_id < 2
+                          puzzleComp=None, outOfBounds=1000, blkOutOfBounds=100):
+        v0 = self.env_id < 2 or self.env_id >= 5   # v3 defaults equal v0's (core.py:149-155)
+        if puzzleComp is None:
+            puzzleComp = 100 if self.env_id >= 5 else 10000
         agentDelta = 10 if agentDelta is None else agentDelta
         agentDistance = (0.1 if v0 else 0.25) if agentDistance is None else agentDistance
         blockDelta = (50 if v0 else 25) if blockDelta is None else blockDelta
@@ -272,7 +276,7 @@ class Batch:
     def render(self, lanes=None, width: int | None = None, height: int | None = None) -> np.ndarray:
         """rgb_array frames of the selected lanes: uint8 [n, height, width, 3] (row 0 = top),
         the reference's render(mode='rgb_array') (multi_robot_puzzle_00.py:528-592)."""
-        w0, h0 = (640, 480) if self.env_id <= 1 else (1440, 810)
+        w0, h0 = (1440, 810) if 2 <= self.env_id <= 4 else (640, 480)   # v0 and v3: 640 x 480
         width, height = width or w0, height or h0
         sel = np.ascontiguousarray(np.arange(self.n_lanes) if lanes is None else np.atleast_1d(lanes), np.int32)
         out = np.zeros((len(sel), height, width, 3), np.uint8)

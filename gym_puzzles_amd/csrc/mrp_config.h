@@ -3,7 +3,8 @@
 //
 // Env ids follow include/mrp.h: 0 MultiRobotPuzzle-v0, 1 MultiRobotPuzzleHeavy-v0,
 // 2 MultiRobotPuzzle-v2, 3 MultiRobotPuzzleHeavy-v2, 4 Heavy-v2 with the build-defined
-// 3-block square.
+// 3-block square, 5 MultiRobotPuzzle-v3 (RobotPuzzleBase,
+// core.py), 6 v3 constructed with heavy=True (tests/test_env.py:12).
 #pragma once
 #include "mrp_math.h"
 
@@ -26,6 +27,9 @@ template <> struct Dims<1> { static constexpr int V = 0, NA = 5, NB = 1, NF = 11
 template <> struct Dims<2> { static constexpr int V = 2, NA = 2, NB = 1, NF = 12, CMAX = 53, OBS = 39, ACT = 4, NDRAW = 7; };
 template <> struct Dims<3> { static constexpr int V = 2, NA = 2, NB = 1, NF = 12, CMAX = 53, OBS = 39, ACT = 4, NDRAW = 7; };
 template <> struct Dims<4> { static constexpr int V = 2, NA = 2, NB = 3, NF = 15, CMAX = 91, OBS = 69, ACT = 4, NDRAW = 9; };
+template <> struct Dims<5> { static constexpr int V = 3, NA = 2, NB = 1, NF = 8, CMAX = 21, OBS = 27, ACT = 6, NDRAW = 7; };
+template <> struct Dims<6> { static constexpr int V = 3, NA = 2, NB = 1, NF = 8, CMAX = 21, OBS = 27, ACT = 6, NDRAW = 7; };
+constexpr int N_ENVS = 7;
 
 // Node pool of a lane's dynamic tree.  b2DynamicTree starts at 16 nodes and doubles only when
 // all are live; a world holds at most 2 * proxies - 1 live nodes, so an env with <= 8 proxies
@@ -65,6 +69,7 @@ struct EnvParams {
     double w_dAgent, w_agentDist, w_dBlock, w_blkDist;
     double shaped_bounds, shaped_blk_bounds, shaped_puzzle;
     double scaled_epsilon;
+    double puzzle_complete;            // v3 puzzle_complete_reward (core.py:155), added as is on completion
 };
 
 }  // namespace mrp

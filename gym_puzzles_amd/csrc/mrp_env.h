@@ -45,10 +45,17 @@ template <int ENV> struct Env : World<ENV> {
 
     // _destroy (multi_robot_puzzle_00.py:218-229): blocks, walls, agents; each body's proxies
     // in fixture-list order (newest first).  The listener is detached, so no End events.
+    // v3 (core.py:246-262): boundary, goal block, agents.
     __device__ __forceinline__ void destroy_bodies() {
         if (!S.haveBodies) return;
         S.cHead = NULLN; S.cFree = 0; S.cCount = 0;
         for (int c = 0; c < D::CMAX; ++c) S.cnext[c] = c + 1 < D::CMAX ? c + 1 : NULLN;
+        if (D::V == 3) {
+            for (int b = ND; b < ND + 4; ++b) for (int k = T.body_nfix[b] - 1; k >= 0; --k) this->destroy_proxy(T.body_fix0[b] + k);
+            for (int b = 0; b < ND; ++b) for (int k = T.body_nfix[b] - 1; k >= 0; --k) this->destroy_proxy(T.body_fix0[b] + k);
+            S.haveBodies = 0;
+            return;
+        }
         for (int b = 0; b < NB; ++b) for (int k = T.body_nfix[b] - 1; k >= 0; --k) this->destroy_proxy(T.body_fix0[b] + k);
         for (int b = ND; b < ND + 4; ++b) for (int k = T.body_nfix[b] - 1; k >= 0; --k) this->destroy_proxy(T.body_fix0[b] + k);
         for (int b = NB; b < ND; ++b) for (int k = T.body_nfix[b] - 1; k >= 0; --k) this->destroy_proxy(T.body_fix0[b] + k);
@@ -73,7 +80,7 @@ template <int ENV> struct Env : World<ENV> {
     // _generate_blocks / _generate_agents / _generate_boundary (+ v2 _set_random_goal)
     __device__ __forceinline__ void create_bodies(const double* d) {
         int k = 0;
-        if (D::V == 0) {
+        if (D::V == 0 || D::V == 3) {   // v3: Block(init_x, init_y, init_angle) then Robots at angle 0
             create_dyn_body(0, (float)d[0], (float)d[1], (float)d[2]);
             k = 3;
             for (int i = 0; i < NA; ++i) { create_dyn_body(NB + i, (float)d[k], (float)d[k + 1], 0.0f); k += 2; }
@@ -100,7 +107,14 @@ template <int ENV> struct Env : World<ENV> {
 
     // _calculate_distance / _calculate_agent_distance
     __device__ __forceinline__ void calc_distances() {
-        if (D::V == 0) {
+        if (D::V == 3) {   // the distances _get_obs stores (core.py:307-343), normalised poses
+            double bx, by; norm_pose(0, bx, by);
+            for (int i = 0; i < NA; ++i) {
+                double ax, ay; norm_pose(NB + i, ax, ay);
+                S.agent_dist[i] = py_distance(ax, ay, bx, by);
+            }
+            S.block_distance[0] = py_distance(bx, by, (S.goal[0][0] - 320.0) / 320.0, (S.goal[0][1] - 240.0) / 320.0);
+        } else if (D::V == 0) {
             for (int b = 0; b < NB; ++b) {
                 float sx = S.cx[b] * 30.0f, sy = S.cy[b] * 30.0f;   // b2Vec2 * SCALE (float32)
                 S.block_distance[b] = py_distance(sx, sy, S.goal[b][0], S.goal[b][1]);
@@ -119,6 +133,12 @@ template <int ENV> struct Env : World<ENV> {
         }
     }
 
+    // RobotPuzzleBase._get_norm_pose (core.py:289-295): (x - ws) / ws, (y - hs) / ws
+    __device__ __forceinline__ void norm_pose(int b, double& x, double& y) const {
+        const double ws = 640 / 30.0 / 2, hs = 480 / 30.0 / 2;
+        x = ((double)S.cx[b] - ws) / ws;
+        y = ((double)S.cy[b] - hs) / ws;
+    }
     __device__ __forceinline__ void unit_vector(int a, int b, double& ux, double& uy) const {   // unitVector :134-138
         double Ax = S.cx[a], Ay = S.cy[a], Bx = S.cx[b], By = S.cy[b];
         double dx = fabs(Bx - Ax), dy = fabs(By - Ay);
@@ -131,8 +151,8 @@ template <int ENV> struct Env : World<ENV> {
     }
 
     __device__ __forceinline__ void apply_actions(const float* act) {
-        if (D::V == 0) {   // multi_robot_puzzle_00.py:415-424
-            const double SPEED = 10.0 / 30.0 * 4;
+        if (D::V == 0 || D::V == 3) {   // multi_robot_puzzle_00.py:415-424; v3 core.py:355-364 + robot.py:65-68
+            const double SPEED = D::V == 3 ? 5.0 : 10.0 / 30.0 * 4;
             for (int i = 0; i < NA; ++i) {
                 int ag = NB + i;
                 float x = act[3 * i], y = act[3 * i + 1], turn = act[3 * i + 2];
@@ -182,7 +202,35 @@ template <int ENV> struct Env : World<ENV> {
         int k = 0;
         bool in_place[NB];
         double reward = 0.0; int done = 0, kind = 0;
-        if (D::V == 0) {
+        if (D::V == 3) {   // _get_obs core.py:297-350, step core.py:369-414
+            const double ws = 640 / 30.0 / 2, hs = 480 / 30.0 / 2;
+            double bx, by; norm_pose(0, bx, by);
+            const double brot = py_mod((double)S.a[0], TWO_PI);
+            for (int i = 0; i < NA; ++i) {
+                double ax, ay; norm_pose(NB + i, ax, ay);
+                obs[k++] = (float)(bx - ax); obs[k++] = (float)(by - ay);
+                obs[k++] = (float)py_mod((double)S.a[NB + i], TWO_PI);
+                obs[k++] = S.goal_contact[i] ? 1.0f : 0.0f;
+            }
+            const double gx = (S.goal[0][0] - 320.0) / 320.0, gy = (S.goal[0][1] - 240.0) / 320.0;
+            obs[k++] = (float)(gx - bx); obs[k++] = (float)(gy - by); obs[k++] = (float)(py_mod(S.goal[0][2], TWO_PI) - brot);
+            Xf xb = this->xf(0);
+            for (int j = 0; j < T.nverts[0]; ++j) {   // Block.get_vertices(norm_fn) blocks.py:118-123
+                V2 wp = mul_xv(xb, T.verts[0][j]);
+                obs[k++] = (float)(((double)wp.x - ws) / ws); obs[k++] = (float)(((double)wp.y - hs) / ws);
+            }
+            const bool in_place0 = S.block_distance[0] <= 25.0 / 640 * 2;
+            double deltaDist = prevB[0] - S.block_distance[0];
+            reward += deltaDist * P.w_dBlock;
+            reward -= P.w_blkDist * S.block_distance[0];
+            for (int i = 0; i < NA; ++i) {
+                double deltaAgent = prevA[i] - S.agent_dist[i];
+                reward += deltaAgent * P.w_dAgent / 4.;
+                reward -= P.w_agentDist * S.agent_dist[i] / 4.;
+                if (S.goal_contact[i]) reward += 0.25;
+            }
+            if (in_place0) { done = 1; kind = 1; reward += P.puzzle_complete; }
+        } else if (D::V == 0) {
             for (int i = 0; i < NA; ++i) {
                 double x = S.cx[0], y = S.cy[0];
                 obs[k++] = (float)((double)S.cx[NB + i] * 30.0 - x * 30.0);

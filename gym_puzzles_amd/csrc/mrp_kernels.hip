@@ -23,7 +23,7 @@
 
 using namespace mrp;
 
-__constant__ EnvTables g_tables[5];
+__constant__ EnvTables g_tables[N_ENVS];
 
 #include "mrp_render.h"
 
@@ -378,6 +378,8 @@ struct mrp_ctx {
     case 2: { constexpr int E = 2; __VA_ARGS__; } break; \
     case 3: { constexpr int E = 3; __VA_ARGS__; } break; \
     case 4: { constexpr int E = 4; __VA_ARGS__; } break; \
+    case 5: { constexpr int E = 5; __VA_ARGS__; } break; \
+    case 6: { constexpr int E = 6; __VA_ARGS__; } break; \
     default: break;                                       \
     }
 
@@ -450,8 +452,8 @@ int mrp_create(int env_id, int n_lanes, int device, uint64_t seed, uint64_t lane
         return MRP_E_HIP;
     };
     if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
-    EnvTables all[5];
-    for (int i = 0; i < 5; ++i) build_tables(i, all[i]);
+    EnvTables all[N_ENVS];
+    for (int i = 0; i < N_ENVS; ++i) build_tables(i, all[i]);
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_tables), all, sizeof(all))) != hipSuccess) return fail("hipMemcpyToSymbol", e);
     if ((e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking)) != hipSuccess) return fail("hipStreamCreate", e);
     ctx->stream = ctx->own_stream;
@@ -504,6 +506,7 @@ int mrp_set_reward_params(mrp_ctx* ctx, double agent_delta, double agent_distanc
     if (!ctx) return MRP_E_ARG;
     ctx->params.w_dAgent = agent_delta; ctx->params.w_agentDist = agent_distance;
     ctx->params.w_dBlock = block_delta; ctx->params.w_blkDist = block_distance;
+    ctx->params.puzzle_complete = puzzle_comp;   // v3 step() adds puzzle_complete_reward itself (core.py:408-410)
     ctx->base_puzzle = puzzle_comp; ctx->base_bounds = out_of_bounds; ctx->base_blk_bounds = blk_out_of_bounds;
     // shaped_* are derived only by update_params() (the reference leaves them undefined until
     // then); the batched default before that call is decay = 1, timestep = 0
@@ -526,7 +529,7 @@ int mrp_update_params(mrp_ctx* ctx, double timestep, double decay) {
 
 int mrp_update_goal(mrp_ctx* ctx, double epoch, double nb_epochs) {
     if (!ctx) return MRP_E_ARG;
-    double eps = ctx->env_id < 2 ? 25.0 : 0.1;
+    double eps = (ctx->env_id < 2 || ctx->env_id >= 5) ? 25.0 : 0.1;   // v3 stores it too (core.py:161-162), unused
     ctx->params.scaled_epsilon = eps * (2 - epoch / nb_epochs);
     return MRP_OK;
 }
@@ -734,8 +737,8 @@ int mrp_debug_progress(int device, uint32_t** host_words, int n_lanes) {
 
 int mrp_debug_velbench(int device, int nc, int pcount, int iters, int blocks, uint64_t* cycles) {
     if (nc < 1 || nc > 16 || pcount < 1 || pcount > 2 || blocks < 1 || !cycles || hipSetDevice(device) != hipSuccess) return MRP_E_ARG;
-    EnvTables all[5];
-    for (int i = 0; i < 5; ++i) build_tables(i, all[i]);
+    EnvTables all[N_ENVS];
+    for (int i = 0; i < N_ENVS; ++i) build_tables(i, all[i]);
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_tables), all, sizeof(all)) != hipSuccess) return MRP_E_HIP;
     unsigned long long* d = nullptr;
     if (hipMalloc((void**)&d, (size_t)blocks * 8) != hipSuccess) return MRP_E_HIP;
@@ -797,7 +800,7 @@ int mrp_debug_trace(int device, uint32_t* out, int n_lanes) {
 // ------------------------------------------------------------------------------ rendering
 static int render_args(mrp_ctx* ctx, int W, int H, mrpr::RenderArgs& A) {
     if (W <= 0 || H <= 0 || (int64_t)W * H > (1 << 24)) return MRP_E_ARG;
-    const bool v0 = ctx->env_id <= 1;
+    const bool v0 = ctx->env_id <= 1 || ctx->env_id >= 5;   // v0 and v3 share the 640x480 px / SCALE 30 viewport
     const double ww = v0 ? 640.0 / 30.0 : 1440.0 / 560.0, wh = v0 ? 480.0 / 30.0 : 810.0 / 560.0;
     A.sx = (float)(ww / W); A.sy = (float)(wh / H);
     A.lw_unit = v0 ? (float)(1.0 / 30.0) : (float)(1.0 / 560.0);

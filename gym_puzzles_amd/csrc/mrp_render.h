@@ -4,6 +4,8 @@
 // Replaces the pyglet/OpenGL `render(mode='rgb_array')` of the reference:
 //   v0 / Heavy-v0 : gym_puzzles/envs/multi_robot_puzzle_00.py:528-592
 //   v2 family     : gym_puzzles/envs/multi_robot_puzzle_02.py:590-661 (_render_human_vision)
+//   v3            : gym_puzzles/envs/core.py:421-459 (+ Block.draw blocks.py:135-152, Robot.draw
+//                   robot.py:76-87)
 // The reference rasterises through OpenGL, which cannot run here; this kernel keeps its
 // scene (draw order, shapes, colours, sizes) and defines the rasteriser exactly: a pixel
 // takes the colour of the LAST primitive in draw order that contains its centre.
@@ -90,7 +92,7 @@ __device__ int build_scene(const LaneState<ENV>& S, const EnvTables& T, const Re
         add_rect(P, n, W - 1.0f - h, 1.0f - h, W - 1.0f + h, H - 1.0f + h, wall);
         add_rect(P, n, 1.0f - h, H - 1.0f - h, W - 1.0f + h, H - 1.0f + h, wall);
         add_rect(P, n, 1.0f - h, 1.0f - h, 1.0f + h, H - 1.0f + h, wall);
-    } else {
+    } else if (D::V == 2) {
         // final points first (_render_human_vision :629-634): white dot, dark-grey ring (linewidth 5)
         for (int b = 0; b < NB; ++b) {
             float fx = (float)(S.goal[b][0] * A.goal_scale), fy = (float)(S.goal[b][1] * A.goal_scale);
@@ -105,7 +107,8 @@ __device__ int build_scene(const LaneState<ENV>& S, const EnvTables& T, const Re
     // [B2 b2Body::CreateFixture], so each body's fixtures are drawn in reverse creation order.
     for (int b = ND; b < ND + 4; ++b)
         for (int k = T.body_nfix[b] - 1; k >= 0; --k) add_poly<ENV>(P, n, T, T.body_fix0[b] + k, T.wall_px[b - ND], T.wall_py[b - ND], 0.0f, 1.0f, wall);
-    const float lg = D::V == 0 ? 0.16f : 0.015f, sm = D::V == 0 ? 0.08f : 0.0075f;
+    // v3: the boundary is its four wall polygons only; Block.draw / Robot.draw use the v0 sizes
+    const float lg = D::V == 2 ? 0.015f : 0.16f, sm = D::V == 2 ? 0.0075f : 0.08f;
     for (int b = 0; b < NB; ++b) {
         for (int k = T.body_nfix[b] - 1; k >= 0; --k) add_poly<ENV>(P, n, T, T.body_fix0[b] + k, S.xpx[b], S.xpy[b], S.xs[b], S.xc[b], grey);
         add_circle(P, n, S.cx[b], S.cy[b], lg, white);
@@ -123,7 +126,7 @@ __device__ int build_scene(const LaneState<ENV>& S, const EnvTables& T, const Re
             add_poly<ENV>(P, n, T, T.body_fix0[b] + k, S.xpx[b], S.xpy[b], S.xs[b], S.xc[b], k > 0 ? grey : white);
         add_circle(P, n, S.xpx[b], S.xpy[b], lg, grey);   // COLORS['i_block']
     }
-    if (D::V == 0) {   // final point, EPSILON/SCALE, blue (:588-590)
+    if (D::V != 2) {   // final point, EPSILON/SCALE, blue (:588-590; v3 core.py:456-457)
         float fx = (float)(S.goal[0][0] * A.goal_scale), fy = (float)(S.goal[0][1] * A.goal_scale);
         add_circle(P, n, fx, fy, 25.0f / 30.0f, blue);
     }

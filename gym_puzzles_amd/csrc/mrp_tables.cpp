@@ -5,7 +5,7 @@
 //
 // Geometry sources: multi_robot_puzzle_00.py:62-67,260-275,299-378 (v0),
 // multi_robot_puzzle_02.py:64-67,313-411 (v2), blocks.py:80-110 (L/I shapes of the
-// build-defined 3-block config).
+// build-defined 3-block config), core.py:186-243 + robot.py:7-44 + blocks.py:70-90 (v3).
 #include "mrp_tables.h"
 
 #include <cmath>
@@ -159,12 +159,13 @@ static FixSpec box_fix(float hx, float hy, float cx, float cy, float density, fl
 }
 
 bool build_tables(int env_id, EnvTables& t) {
-    if (env_id < 0 || env_id > 4) return false;
+    if (env_id < 0 || env_id >= N_ENVS) return false;
     std::memset(&t, 0, sizeof(t));
-    static const int NA[5] = {2, 5, 2, 2, 2}, NB[5] = {1, 1, 1, 1, 3};
-    static const int OBS[5] = {28, 40, 39, 39, 69}, ACT[5] = {6, 15, 4, 4, 4}, NDRAW[5] = {7, 13, 7, 7, 9};
-    static const int MAXSTEPS[5] = {2000, 3000, 2000, 2000, 2000};
-    t.env_id = env_id; t.version = env_id < 2 ? 0 : 2;
+    static const int NA[N_ENVS] = {2, 5, 2, 2, 2, 2, 2}, NB[N_ENVS] = {1, 1, 1, 1, 3, 1, 1};
+    static const int OBS[N_ENVS] = {28, 40, 39, 39, 69, 27, 27}, ACT[N_ENVS] = {6, 15, 4, 4, 4, 6, 6};
+    static const int NDRAW[N_ENVS] = {7, 13, 7, 7, 9, 7, 7};
+    static const int MAXSTEPS[N_ENVS] = {2000, 3000, 2000, 2000, 2000, 1500, 1500};
+    t.env_id = env_id; t.version = env_id < 2 ? 0 : (env_id < 5 ? 2 : 3);
     t.n_agents = NA[env_id]; t.n_blocks = NB[env_id];
     t.n_dyn = t.n_agents + t.n_blocks; t.n_bodies = t.n_dyn + 4;
     t.obs_dim = OBS[env_id]; t.act_dim = ACT[env_id]; t.n_draws = NDRAW[env_id]; t.max_steps = MAXSTEPS[env_id];
@@ -198,6 +199,39 @@ bool build_tables(int env_id, EnvTables& t) {
         t.draw_lo[k] = xr[0]; t.draw_hi[k++] = xr[1]; t.draw_lo[k] = yr[0]; t.draw_hi[k++] = yr[1];
         t.draw_lo[k] = 0.0; t.draw_hi[k++] = 2 * PI;
         for (int i = 0; i < t.n_agents; ++i) { t.draw_lo[k] = xr[0]; t.draw_hi[k++] = xr[1]; t.draw_lo[k] = yr[0]; t.draw_hi[k++] = yr[1]; }
+        t.agent_angle = 0.0f;
+    } else if (t.version == 3) {
+        // RobotPuzzleBase: Block("T") at scale 0.5 (heavy: 1) density 5 (heavy: 10), friction 2.5,
+        // damping 5 (blocks.py:70-90, core.py:204-225); Robot AGENT_POLY * 8, density 5,
+        // friction 0.2, no damping (robot.py:34-44); walls as v0 (core.py:186-201)
+        const bool heavy = env_id == 6;
+        const double sc = heavy ? 1.0 : 0.5, dense = heavy ? 5.0 * 2 : 5.0;
+        FixSpec blk[2] = {box_fix((float)(1 * sc), (float)(1 * sc), 0.0f, (float)(-1 * sc), (float)dense, 2.5f),
+                          box_fix((float)(3 * sc), (float)(1 * sc), 0.0f, (float)(1 * sc), (float)dense, 2.5f)};
+        add_body(t, 0, nfix, blk, 2, true, 5.0f);
+        save_vertices(t, 0, blk, 2);
+        static const double AP[8][2] = {{-0.039, -0.095}, {0.039, -0.095}, {0.095, -0.039}, {0.095, 0.039},
+                                        {0.039, 0.095}, {-0.039, 0.095}, {-0.095, 0.039}, {-0.095, -0.039}};
+        V2 poly[8];
+        for (int i = 0; i < 8; ++i) poly[i] = v2((float)(AP[i][0] * 8.0), (float)(AP[i][1] * 8.0));
+        FixSpec ag; std::memset(&ag, 0, sizeof(ag));
+        poly_set(ag.shape, poly, 8); ag.density = 5.0f; ag.friction = 0.2f;
+        for (int i = 0; i < t.n_agents; ++i) add_body(t, 1 + i, nfix, &ag, 1, true, 0.0f);
+        const double vw = 640 / 30.0, vh = 480 / 30.0;
+        const double bx[4] = {0, 1, 0.5, 0.5}, by[4] = {0.5, 0.5, 0, 1};
+        for (int w = 0; w < 4; ++w) {
+            FixSpec wf; std::memset(&wf, 0, sizeof(wf));
+            poly_box(wf.shape, (float)(w < 2 ? 1.0 : vw), (float)(w < 2 ? vh : 1.0)); wf.density = 0.0f; wf.friction = 0.2f;
+            int b = t.n_dyn + w;
+            add_body(t, b, nfix, &wf, 1, false, 0.0f);
+            t.wall_px[w] = (float)(vw * bx[w]); t.wall_py[w] = (float)(vh * by[w]);
+        }
+        t.goal_x = 5.0 / 6.0 * 640 - 4.0 / 3.0 * 1; t.goal_y = (double)(480 / 2); t.goal_a = 0.0;   // core.py:277-281
+        int k = 0;   // core.py:212-215, 231-232
+        t.draw_lo[k] = vw / 3 + 2 * 1; t.draw_hi[k++] = vw * 2 / 3 - 2 * 1;
+        t.draw_lo[k] = 3 * 1; t.draw_hi[k++] = vh - 3 * 1;
+        t.draw_lo[k] = 0.0; t.draw_hi[k++] = 2 * PI;
+        for (int i = 0; i < t.n_agents; ++i) { t.draw_lo[k] = 1; t.draw_hi[k++] = vw / 3 - 2 * 1; t.draw_lo[k] = 1; t.draw_hi[k++] = vh - 1; }
         t.agent_angle = 0.0f;
     } else {
         const bool heavy = env_id >= 3;
@@ -245,13 +279,14 @@ bool build_tables(int env_id, EnvTables& t) {
 }
 
 void default_params(int env_id, EnvParams& p) {
-    if (env_id < 2) {   // set_reward_params defaults multi_robot_puzzle_00.py:231-239
+    if (env_id < 2 || env_id >= 5) {   // set_reward_params defaults multi_robot_puzzle_00.py:231-239, core.py:149-155
         p.w_dAgent = 10; p.w_agentDist = 0.1; p.w_dBlock = 50; p.w_blkDist = 0.025; p.scaled_epsilon = 25.0;
     } else {            // multi_robot_puzzle_02.py:216-225, EPSILON :58
         p.w_dAgent = 10; p.w_agentDist = 0.25; p.w_dBlock = 25; p.w_blkDist = 0.1; p.scaled_epsilon = 0.1;
     }
     // update_params(timestep=0, decay=1) values; the reference leaves these undefined until called
     p.shaped_bounds = 1000.0; p.shaped_blk_bounds = 100.0; p.shaped_puzzle = 10000.0;
+    p.puzzle_complete = 100.0;
 }
 
 }  // namespace mrp

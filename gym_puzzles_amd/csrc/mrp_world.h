@@ -455,6 +455,8 @@ template <int ENV> struct World {
 
     // ------------------------------------------------------------------ contacts
     __device__ __forceinline__ void contact_event(int c, int value) {   // ContactDetector (multi_robot_puzzle_00.py:92-111)
+        // v3's detector (core.py:46-61) compares Robot wrappers with b2Body objects: never a match
+        if (D::V == 3) return;
         int bA = L.fix_body[S.cfa[c]], bB = L.fix_body[S.cfb[c]];
         for (int i = 0; i < NA; ++i) {
             int ag = NB + i;

@@ -6,6 +6,7 @@ reference (``gym_puzzles/envs/__init__.py``):
     MultiRobotPuzzle, MultiRobotPuzzleHeavy          multi_robot_puzzle_00.py:142,606
     MultiRobotPuzzle2, MultiRobotPuzzleHeavy2        multi_robot_puzzle_02.py:126,711
     MultiRobotPuzzleHeavy2ThreeBlock                 build-defined 3-block config
+    RobotPuzzleBase                                  core.py:77 (MultiRobotPuzzle-v3; heavy=True too)
 
 Each instance is ONE lane of a device batch (``mrp_ctx`` with n_lanes = 1); the physics runs
 on the GPU and the class only moves one row of inputs/outputs.  For thousands of lanes use
@@ -49,7 +50,8 @@ class _MRPBase:
         self.done_status = None
         self._params_updated = False
         self.set_reward_params()
-        self.observation_space = make_box(-self._obs_high(), self._obs_high(), dtype=np.float32)
+        low, high = self._obs_bounds()
+        self.observation_space = make_box(low, high, dtype=np.float32)
         self.action_space = make_box(-np.ones(self._b.act_dim), np.ones(self._b.act_dim), dtype=np.float32)
         self.reset()
 
@@ -137,6 +139,9 @@ class _MRPBase:
     def _obs_high(self):
         raise NotImplementedError
 
+    def _obs_bounds(self):
+        return -self._obs_high(), self._obs_high()
+
     @property
     def blks_in_place(self):
         return int(self._b.flags()[0, -1])
@@ -208,13 +213,66 @@ class MultiRobotPuzzleHeavy2ThreeBlock(MultiRobotPuzzle2):
     heavy = True
 
 
+class RobotPuzzleBase(_MRPBase):
+    """core.py:77-418 (MultiRobotPuzzle-v3): holonomic Robots (robot.py:17-73) pushing a T Block
+    (blocks.py:17-132) towards a fixed goal; normalised observations.  ``heavy=True`` is the
+    reference test's configuration (tests/test_env.py:12): T block at scale 1, density 10.
+
+    Reference quirks kept: the contact detector never sets ``goal_contact`` (core.py:46-61 compares
+    Robot wrappers with b2Body objects), so that observation entry and the +0.25 bonus stay 0;
+    ``update_params`` / ``update_goal`` store values step() never reads; completion adds
+    ``puzzle_complete_reward`` unshaped (core.py:408-410)."""
+    env_id = 5
+
+    def __init__(self, num_agents: int = 2, goal_velocity: float = 1.5, block_density: float = 5.0,
+                 heavy: bool = False, hardmode: bool = False, device: int = 0):
+        if num_agents != 2:
+            raise NotImplementedError("the device build covers num_agents=2 (the registered config)")
+        self.env_id = 6 if heavy else 5
+        self.goal_velocity = goal_velocity
+        self.heavy = heavy
+        self.hardmode = hardmode
+        super().__init__(device)
+
+    def set_reward_params(self, agentDelta=10, agentDistance=0.1, blockDelta=50, blockDistance=0.025, puzzleComp=100):
+        self.weight_deltaAgent = agentDelta
+        self.weight_agent_dist = agentDistance
+        self.weight_deltaBlock = blockDelta
+        self.weight_blk_dist = blockDistance
+        self.puzzle_complete_reward = puzzleComp
+        self._b.set_reward_params(agentDelta, agentDistance, blockDelta, blockDistance, puzzleComp)
+
+    def update_params(self, timestep, decay):   # core.py:158-159: stored, never read by step()
+        self.shaped_puzzle_reward = self.puzzle_complete_reward * decay ** (-timestep)
+
+    def update_goal(self, epoch, nb_epochs):    # core.py:161-162: stored, never read by step()
+        self.scaled_epsilon = 25.0 * (2 - epoch / nb_epochs)
+
+    def _needs_shaped(self):
+        return False
+
+    def _return_status(self):
+        return self.done_status if self.done_status else "Stayed in bounds"
+
+    def _obs_bounds(self):   # core.py:121-132
+        n = self._b.n_agents
+        high = [2.5, 2.5, 2 * np.pi, 1.0] * n + [2.5, 2.5, 2 * np.pi] + [1.5] * 16
+        low = [-2.5, -2.5, -2 * np.pi, 0.0] * n + [-2.5, -2.5, -2 * np.pi] + [-1.5] * 16
+        return np.array(low), np.array(high)
+
+    def _obs_high(self):
+        return self._obs_bounds()[1]
+
+
 ENV_CLASSES = {
     "MultiRobotPuzzle-v0": (MultiRobotPuzzle, 2000),
     "MultiRobotPuzzleHeavy-v0": (MultiRobotPuzzleHeavy, 3000),
     "MultiRobotPuzzle-v2": (MultiRobotPuzzle2, 2000),
     "MultiRobotPuzzleHeavy-v2": (MultiRobotPuzzleHeavy2, 2000),
     "MultiRobotPuzzleHeavy-v2-3block": (MultiRobotPuzzleHeavy2ThreeBlock, 2000),
+    "MultiRobotPuzzle-v3": (RobotPuzzleBase, 1500),
 }
+REWARD_THRESHOLD = {"MultiRobotPuzzle-v3": 110}   # __init__.py:35; the others register 500
 
 
 class TimeLimit:
@@ -262,5 +320,5 @@ def register_with_gym() -> bool:
         return False
     for name, (cls, max_steps) in ENV_CLASSES.items():
         register(id=name + "-mi355x", entry_point=f"gym_puzzles_amd.envs:{cls.__name__}",
-                 max_episode_steps=max_steps, reward_threshold=500)
+                 max_episode_steps=max_steps, reward_threshold=REWARD_THRESHOLD.get(name, 500))
     return True

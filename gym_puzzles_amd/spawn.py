@@ -10,6 +10,7 @@
   per agent, then goal x, y (``_set_random_goal``; SIMPLE=True places the block at the
   screen centre and fixes agent heading at 3/2*pi).
 * 3-block (build-defined): one angle per block (T, L, I), agents, goal.
+* v3 / v3 heavy (``core.py:212-215,231-232``): block x, y, angle, then x, y per agent.
 """
 from __future__ import annotations
 
@@ -20,8 +21,11 @@ _V0_SCALE, _V0_W, _V0_H, _V0_BORDER = 30.0, 640, 480, 1
 # v2 constants (multi_robot_puzzle_02.py:39-44, 305)
 _V2_SCALE, _V2_W, _V2_H, _V2_BORDER, _V2_GOAL_BORDER = 140.0 * 4, 1440, 810, 0.3, 0.4
 
-N_AGENTS = {0: 2, 1: 5, 2: 2, 3: 2, 4: 2}
-N_BLOCKS = {0: 1, 1: 1, 2: 1, 3: 1, 4: 3}
+# v3 constants (core.py:16-19, 97-98)
+_V3_SCALE, _V3_W, _V3_H, _V3_BORDER = 30.0, 640, 480, 1
+
+N_AGENTS = {0: 2, 1: 5, 2: 2, 3: 2, 4: 2, 5: 2, 6: 2}
+N_BLOCKS = {0: 1, 1: 1, 2: 1, 3: 1, 4: 3, 5: 1, 6: 1}
 
 
 def draw_bounds(env_id: int):
@@ -32,6 +36,10 @@ def draw_bounds(env_id: int):
         yr = (_V0_BORDER, _V0_H / _V0_SCALE - _V0_BORDER)
         b += [xr, yr, (0, 2 * np.pi)]
         b += [xr, yr] * N_AGENTS[env_id]
+    elif env_id in (5, 6):
+        b += [(_V3_W / _V3_SCALE / 3 + 2 * _V3_BORDER, _V3_W / _V3_SCALE * 2 / 3 - 2 * _V3_BORDER),
+              (3 * _V3_BORDER, _V3_H / _V3_SCALE - 3 * _V3_BORDER), (0, 2 * np.pi)]
+        b += [(_V3_BORDER, _V3_W / _V3_SCALE / 3 - 2 * _V3_BORDER), (_V3_BORDER, _V3_H / _V3_SCALE - _V3_BORDER)] * N_AGENTS[env_id]
     else:
         b += [(0, 2 * np.pi)] * N_BLOCKS[env_id]
         xr = (_V2_BORDER, _V2_W / _V2_SCALE / 3 - _V2_BORDER)

@@ -21,7 +21,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from ._native import Batch, env_dims
+from ._native import ENV_IDS, Batch, env_dims
 from .seeding import make_box
 
 try:   # SB3 1.x/2.x: VecEnv(num_envs, observation_space, action_space)
@@ -29,8 +29,7 @@ try:   # SB3 1.x/2.x: VecEnv(num_envs, observation_space, action_space)
 except ImportError:
     _VecEnvBase = object
 
-_ID = {"MultiRobotPuzzle-v0": 0, "MultiRobotPuzzleHeavy-v0": 1, "MultiRobotPuzzle-v2": 2,
-       "MultiRobotPuzzleHeavy-v2": 3, "MultiRobotPuzzleHeavy-v2-3block": 4}
+_ID = dict(ENV_IDS)
 
 
 class MultiRobotPuzzleVecEnv(_VecEnvBase):

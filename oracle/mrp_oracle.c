@@ -56,14 +56,16 @@ double or_rng_u01(uint64_t seed, uint64_t lane, uint64_t stream, uint64_t counte
 
 /* ---------------------------------------------------------------- configs (BASELINE.json configs) */
 typedef struct { int version, n_agents, n_blocks, heavy, obs_dim, act_dim, n_draws, max_steps; } Cfg;
-static const Cfg CFGS[5] = {
+static const Cfg CFGS[7] = {
     {0, 2, 1, 0, 28, 6, 7, 2000},   /* MultiRobotPuzzle-v0        __init__.py:3-8 */
     {0, 5, 1, 1, 40, 15, 13, 3000}, /* MultiRobotPuzzleHeavy-v0   __init__.py:10-15 */
     {2, 2, 1, 0, 39, 4, 7, 2000},   /* MultiRobotPuzzle-v2        __init__.py:17-22 */
     {2, 2, 1, 1, 39, 4, 7, 2000},   /* MultiRobotPuzzleHeavy-v2   __init__.py:24-29 */
     {2, 2, 3, 1, 69, 4, 9, 2000},   /* Heavy-v2, 3-block square (build-defined) */
+    {3, 2, 1, 0, 27, 6, 7, 1500},   /* MultiRobotPuzzle-v3 (RobotPuzzleBase)  __init__.py:31-35 */
+    {3, 2, 1, 1, 27, 6, 7, 1500},   /* MultiRobotPuzzle-v3 with heavy=True (tests/test_env.py:12) */
 };
-static int valid(int id) { return id >= 0 && id < 5; }
+static int valid(int id) { return id >= 0 && id < 7; }
 int or_obs_dim(int id) { return valid(id) ? CFGS[id].obs_dim : -1; }
 int or_act_dim(int id) { return valid(id) ? CFGS[id].act_dim : -1; }
 int or_n_draws(int id) { return valid(id) ? CFGS[id].n_draws : -1; }
@@ -94,6 +96,19 @@ int or_max_episode_steps(int id) { return valid(id) ? CFGS[id].max_steps : -1; }
 #define V2_FORCE 0.75
 #define V2_EPSILON 0.1
 
+/* v3 constants core.py:16-36, robot.py:7-15, blocks.py:10-13 */
+#define V3_SCALE 30.0
+#define V3_VW 640
+#define V3_VH 480
+#define V3_BORDER 1.0
+#define V3_BLK_FR 2.5
+#define V3_DAMP 5.0
+#define V3_DENSE 5.0
+#define V3_EPSILON 25.0
+#define V3_AGT_SCALE 8.0
+#define V3_AGT_DENSE 5.0
+#define V3_MAX_SPEED 5.0
+
 static const double PY_PI = 3.141592653589793;
 
 struct OrEnv {
@@ -110,11 +125,14 @@ struct OrEnv {
     double scaled_epsilon;
     double w_dAgent, w_agentDist, w_dBlock, w_blkDist;
     double shaped_bounds, shaped_blk_bounds, shaped_puzzle;
+    double puzzle_complete;      /* v3 puzzle_complete_reward (core.py:155; step() adds it directly) */
 };
 
 /* ContactDetector.BeginContact/EndContact: multi_robot_puzzle_00.py:92-111, _02.py:85-102.
  * Last event wins per agent; wall flag is written but never read by obs/reward. */
 static void on_contact(OrEnv* e, Contact* c, int value) {
+    if (e->cfg.version == 3) return;   /* core.py:46-61 tests `agent in [fixtureA.body, ...]` with Robot
+                                          wrappers against b2Body objects: never true, flags stay False */
     Body* bA = c->fA->body; Body* bB = c->fB->body;
     Body* goal = e->blocks[0];
     for (int i = 0; i < e->cfg.n_agents; ++i) {
@@ -140,12 +158,19 @@ OrEnv* or_create(int env_id) {
         e->goal[0][0] = (double)(V0_VW / 2) + 0.0 * V0_SCALE;
         e->goal[0][1] = (double)(V0_VH / 2) + 0.75 * V0_SCALE;
         e->goal[0][2] = 0.0;
+    } else if (e->cfg.version == 3) {   /* core.py:149-155 set_reward_params defaults; goal core.py:277-281 */
+        e->w_dAgent = 10; e->w_agentDist = 0.1; e->w_dBlock = 50; e->w_blkDist = 0.025;
+        e->scaled_epsilon = V3_EPSILON;
+        e->goal[0][0] = 5.0 / 6.0 * (double)V3_VW - 4.0 / 3.0 * V3_BORDER;
+        e->goal[0][1] = (double)(V3_VH / 2);
+        e->goal[0][2] = 0.0;
     } else {                         /* _02.py:216-225 */
         e->w_dAgent = 10; e->w_agentDist = 0.25; e->w_dBlock = 25; e->w_blkDist = 0.1;
         e->scaled_epsilon = V2_EPSILON;
     }
     /* shaped_* only exist after update_params() (_02.py:227-230); default = decay 1, t 0 */
     e->shaped_bounds = 1000.0; e->shaped_blk_bounds = 100.0; e->shaped_puzzle = 10000.0;
+    e->puzzle_complete = 100.0;
     return e;
 }
 
@@ -157,6 +182,13 @@ void or_destroy(OrEnv* e) { if (!e) return; b2o_world_destroy(e->world); free(e)
 static void env_destroy_bodies(OrEnv* e) {
     if (!e->have_bodies) return;
     b2o_set_listener(e->world, NULL, NULL, NULL);
+    if (e->cfg.version == 3) {   /* core.py:246-262: boundary, goal block, agents */
+        for (int i = 0; i < 4; ++i) b2o_destroy_body(e->world, e->walls[i]);
+        for (int i = 0; i < e->cfg.n_blocks; ++i) b2o_destroy_body(e->world, e->blocks[i]);
+        for (int i = 0; i < e->cfg.n_agents; ++i) b2o_destroy_body(e->world, e->agents[i]);
+        e->have_bodies = 0;
+        return;
+    }
     for (int i = 0; i < e->cfg.n_blocks; ++i) b2o_destroy_body(e->world, e->blocks[i]);
     for (int i = 0; i < 4; ++i) b2o_destroy_body(e->world, e->walls[i]);
     for (int i = 0; i < e->cfg.n_agents; ++i) b2o_destroy_body(e->world, e->agents[i]);
@@ -224,6 +256,50 @@ static void gen_v0(OrEnv* e, const double* d) {
         double hx = i < 2 ? 1.0 : (double)V0_VW / V0_SCALE;
         double hy = i < 2 ? (double)V0_VH / V0_SCALE : 1.0;
         BodyDef bd = { BT_STATIC, { (float)((double)V0_VW / V0_SCALE * bx[i]), (float)((double)V0_VH / V0_SCALE * by[i]) }, 0.0f, 0.0f, 0.0f, 100 + i };
+        Body* b = b2o_create_body(e->world, &bd);
+        Poly p; b2o_poly_box(&p, (float)hx, (float)hy);
+        FixtureDef fd = { &p, 0.0f, 0.2f, 0.0f, 0 };
+        b2o_create_fixture(b, &fd);
+        e->walls[i] = b;
+    }
+}
+
+/* RobotPuzzleBase._generate_blocks / _generate_agents / _generate_boundary (core.py:186-243) with
+ * Block(shape="T") (blocks.py:68-90) and Robot (robot.py:17-47).  A new Block instance per reset:
+ * its vertex list is rebuilt every time (same content). */
+static void gen_v3(OrEnv* e, const double* d) {
+    const double scale = e->cfg.heavy ? 1.0 : 0.5;            /* core.py:205-210 */
+    const double blk_dense = e->cfg.heavy ? V3_DENSE * 2 : V3_DENSE;
+    int k = 0;
+    {
+        BodyDef bd = { BT_DYNAMIC, { (float)d[k], (float)d[k + 1] }, (float)d[k + 2], (float)V3_DAMP, (float)V3_DAMP, 0 };
+        k += 3;
+        Body* b = b2o_create_body(e->world, &bd);
+        add_box_fixture(b, (float)(1 * scale), (float)(1 * scale), 0.0f, (float)(-1 * scale), (float)blk_dense, (float)V3_BLK_FR, 0);
+        add_box_fixture(b, (float)(3 * scale), (float)(1 * scale), 0.0f, (float)(1 * scale), (float)blk_dense, (float)V3_BLK_FR, 1);
+        e->blocks[0] = b;
+        e->nverts[0] = 0; e->verts_init[0] = 0;
+        save_vertices(e, 0);
+    }
+    /* AGENT_POLY robot.py:7-10 scaled by 8 (Python floats, then b2Vec2) */
+    static const double AP[8][2] = { { -0.039, -0.095 }, { 0.039, -0.095 }, { 0.095, -0.039 }, { 0.095, 0.039 },
+                                     { 0.039, 0.095 }, { -0.039, 0.095 }, { -0.095, 0.039 }, { -0.095, -0.039 } };
+    V2 poly[8];
+    for (int i = 0; i < 8; ++i) { poly[i].x = (float)(AP[i][0] * V3_AGT_SCALE); poly[i].y = (float)(AP[i][1] * V3_AGT_SCALE); }
+    Poly ap; b2o_poly_set(&ap, poly, 8);
+    for (int i = 0; i < e->cfg.n_agents; ++i) {
+        BodyDef bd = { BT_DYNAMIC, { (float)d[k], (float)d[k + 1] }, 0.0f, 0.0f, 0.0f, 10 + i };   /* no damping (robot.py:42-43) */
+        k += 2;
+        Body* b = b2o_create_body(e->world, &bd);
+        FixtureDef fd = { &ap, (float)V3_AGT_DENSE, 0.2f, 0.0f, 0 };   /* fixtureDef: density 5, friction default 0.2 */
+        b2o_create_fixture(b, &fd);
+        e->agents[i] = b; e->goal_contact[i] = 0;
+    }
+    const double bx[4] = { 0, 1, 0.5, 0.5 }, by[4] = { 0.5, 0.5, 0, 1 };
+    for (int i = 0; i < 4; ++i) {   /* _generate_boundary core.py:186-201, thickness BORDER */
+        double hx = i < 2 ? V3_BORDER : (double)V3_VW / V3_SCALE;
+        double hy = i < 2 ? (double)V3_VH / V3_SCALE : V3_BORDER;
+        BodyDef bd = { BT_STATIC, { (float)((double)V3_VW / V3_SCALE * bx[i]), (float)((double)V3_VH / V3_SCALE * by[i]) }, 0.0f, 0.0f, 0.0f, 100 + i };
         Body* b = b2o_create_body(e->world, &bd);
         Poly p; b2o_poly_box(&p, (float)hx, (float)hy);
         FixtureDef fd = { &p, 0.0f, 0.2f, 0.0f, 0 };
@@ -300,7 +376,24 @@ static void gen_v2(OrEnv* e, const double* d) {
 }
 
 /* _calculate_distance / _calculate_agent_distance: v0 :277-291, v2 _02.py:263-277 */
+/* RobotPuzzleBase._get_norm_pose (core.py:289-295): x, y over width_scale, angle mod 2 pi */
+static void v3_norm_pose(const Body* b, double* x, double* y) {
+    const double ws = (double)V3_VW / V3_SCALE / 2, hs = (double)V3_VH / V3_SCALE / 2;
+    *x = ((double)b->sweep.c.x - ws) / ws;
+    *y = ((double)b->sweep.c.y - hs) / ws;
+}
 static void calc_distances(OrEnv* e) {
+    if (e->cfg.version == 3) {   /* the distances _get_obs (core.py:297-350) stores */
+        double bx, by; v3_norm_pose(e->blocks[0], &bx, &by);
+        for (int i = 0; i < e->cfg.n_agents; ++i) {
+            double ax, ay; v3_norm_pose(e->agents[i], &ax, &ay);
+            e->agent_dist[i] = py_distance(ax, ay, bx, by);
+        }
+        double gx = (e->goal[0][0] - (double)V3_VW / 2) / ((double)V3_VW / 2);
+        double gy = (e->goal[0][1] - (double)V3_VH / 2) / ((double)V3_VW / 2);
+        e->block_distance[0] = py_distance(bx, by, gx, gy);
+        return;
+    }
     if (e->cfg.version == 0) {
         for (int bi = 0; bi < e->cfg.n_blocks; ++bi) {
             V2 c = e->blocks[bi]->sweep.c;
@@ -338,6 +431,18 @@ static void unit_vector(const Body* a, const Body* b, double* ux, double* uy) {
 
 static void apply_actions(OrEnv* e, const float* action) {
     Body* goal = e->blocks[0];
+    if (e->cfg.version == 3) {   /* core.py:353-364, Robot.step robot.py:65-68 */
+        for (int i = 0; i < e->cfg.n_agents; ++i) {
+            Body* ag = e->agents[i];
+            float x = action[3 * i], y = action[3 * i + 1], turn = action[3 * i + 2];
+            b2o_set_linear_velocity(ag, (V2){ (float)((double)x * V3_MAX_SPEED), (float)((double)y * V3_MAX_SPEED) });
+            b2o_set_angular_velocity(ag, (float)(double)turn);
+            double force = py_pow(1.1, -e->agent_dist[i]);
+            double ux, uy; unit_vector(ag, goal, &ux, &uy);
+            b2o_apply_force(goal, (V2){ (float)(force * ux), (float)(force * uy) }, goal->sweep.c);   /* Block.apply_soft_force */
+        }
+        return;
+    }
     if (e->cfg.version == 0) {
         const double SPEED = 10.0 / V0_SCALE * 4;   /* :50 */
         for (int i = 0; i < e->cfg.n_agents; ++i) {   /* :415-424 */
@@ -387,7 +492,38 @@ static void build_obs_and_reward(OrEnv* e, const double* prev_agent, const doubl
     Body* goal = e->blocks[0];
     int in_place[3];
     double reward = 0.0; int done = 0, kind = 0;
-    if (cfg->version == 0) {
+    if (cfg->version == 3) {
+        /* _get_obs core.py:297-350 */
+        const double ws = (double)V3_VW / V3_SCALE / 2, hs = (double)V3_VH / V3_SCALE / 2;
+        double bx, by; v3_norm_pose(goal, &bx, &by);
+        double brot = py_mod((double)goal->sweep.a, TWO_PI);
+        for (int i = 0; i < cfg->n_agents; ++i) {
+            double ax, ay; v3_norm_pose(e->agents[i], &ax, &ay);
+            double arot = py_mod((double)e->agents[i]->sweep.a, TWO_PI);
+            obs[k++] = bx - ax; obs[k++] = by - ay; obs[k++] = arot;
+            obs[k++] = e->goal_contact[i] ? 1.0 : 0.0;
+        }
+        double gx = (e->goal[0][0] - (double)V3_VW / 2) / ((double)V3_VW / 2);
+        double gy = (e->goal[0][1] - (double)V3_VH / 2) / ((double)V3_VW / 2);
+        double grot = py_mod(e->goal[0][2], TWO_PI);
+        obs[k++] = gx - bx; obs[k++] = gy - by; obs[k++] = grot - brot;
+        for (int j = 0; j < e->nverts[0]; ++j) {   /* Block.get_vertices with norm_fn */
+            V2 wp = b2o_world_point(goal, e->verts[0][j]);
+            obs[k++] = ((double)wp.x - ws) / ws; obs[k++] = ((double)wp.y - hs) / ws;
+        }
+        /* step core.py:369-414 */
+        int in_place0 = e->block_distance[0] <= V3_EPSILON / (double)V3_VW * 2;
+        double deltaDist = prev_block[0] - e->block_distance[0];
+        reward += deltaDist * e->w_dBlock;
+        reward -= e->w_blkDist * e->block_distance[0];
+        for (int i = 0; i < cfg->n_agents; ++i) {
+            double deltaAgent = prev_agent[i] - e->agent_dist[i];
+            reward += deltaAgent * e->w_dAgent / 4.;
+            reward -= e->w_agentDist * e->agent_dist[i] / 4.;
+            if (e->goal_contact[i]) reward += 0.25;
+        }
+        if (in_place0) { done = 1; kind = 1; reward += e->puzzle_complete; }
+    } else if (cfg->version == 0) {
         /* obs :442-472 */
         for (int i = 0; i < cfg->n_agents; ++i) {
             double x = goal->sweep.c.x, y = goal->sweep.c.y;
@@ -509,7 +645,7 @@ void or_step(OrEnv* e, const float* action, double* obs, double* reward, int* do
 void or_reset(OrEnv* e, const double* draws, const float* reset_action, double* obs_out) {
     env_destroy_bodies(e);
     b2o_set_listener(e->world, cb_begin, cb_end, e);
-    if (e->cfg.version == 0) gen_v0(e, draws); else gen_v2(e, draws);
+    if (e->cfg.version == 0) gen_v0(e, draws); else if (e->cfg.version == 3) gen_v3(e, draws); else gen_v2(e, draws);
     e->have_bodies = 1;
     calc_distances(e);
     double reward; int done, kind;

@@ -26,6 +26,8 @@ ENV_IDS = {
     "MultiRobotPuzzle-v2": 2,
     "MultiRobotPuzzleHeavy-v2": 3,
     "MultiRobotPuzzleHeavy-v2-3block": 4,
+    "MultiRobotPuzzle-v3": 5,
+    "MultiRobotPuzzle-v3-heavy": 6,
 }
 
 

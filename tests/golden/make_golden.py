@@ -16,6 +16,8 @@
    MultiRobotPuzzle-v0: env construction runs reset() once (multi_robot_puzzle_00.py:209) with
    whatever the global RNG holds (here: np.random.seed(0) before construction), then
    np.random.seed(17), action_space.seed(17), reset(), and 200 steps of action_space.sample().
+4. ``scenario_v3heavy_seed17.npz`` -- the same test file's actual target, MultiRobotPuzzle-v3 with
+   heavy=True (test_env.py:12-36): two resets, then steps until done or the 1500-step TimeLimit.
 """
 from __future__ import annotations
 
@@ -38,7 +40,7 @@ LANES, STEPS = 4, 64
 
 def spawn_fixture():
     out = {}
-    for env_id in range(5):
+    for env_id in range(7):
         for seed in (0, 17, 2021):
             np.random.seed(seed)
             d = reference_draws(env_id)          # global np.random, like the reference
@@ -105,9 +107,42 @@ def scenario_v0():
                         obs=obs, reward=rew, bodies=o.bodies())
 
 
+def scenario_v3_heavy():
+    """gym_puzzles/tests/test_env.py itself: gym.make('MultiRobotPuzzle-v3', heavy=True) (the
+    constructor's reset() draws from whatever the global RNG holds -- np.random.seed(0) here),
+    np.random.seed(17), env.seed(17), action_space.seed(17), obs = env.reset(), then for the first
+    of its 5 episodes env.reset() and action_space.sample() steps until done (TimeLimit 1500;
+    `done` is never cleared, so the later episodes run no steps)."""
+    env_id, limit = 6, 1500
+    o = OracleEnv(env_id)
+    sp = Box(-1.0, 1.0, shape=(o.act_dim,))
+    np.random.seed(0)
+    o.reset(reference_draws(env_id), sp.sample())
+    np.random.seed(17)
+    sp.seed(17)
+    d1 = reference_draws(env_id)
+    a1 = sp.sample()
+    obs1 = o.reset(d1, a1).astype(np.float32)
+    d2 = reference_draws(env_id)
+    a2 = sp.sample()
+    obs2 = o.reset(d2, a2).astype(np.float32)
+    acts, obs, rew, done = [], [], [], []
+    for t in range(limit):
+        a = sp.sample()
+        ob, r, dn, _ = o.step(a)
+        acts.append(a); obs.append(ob.astype(np.float32)); rew.append(r); done.append(dn)
+        if dn:
+            break
+    np.savez_compressed(os.path.join(HERE, "scenario_v3heavy_seed17.npz"), draws=np.stack([d1, d2]),
+                        act0=np.stack([a1, a2]), obs0=np.stack([obs1, obs2]), acts=np.array(acts, np.float32),
+                        obs=np.array(obs, np.float32), reward=np.array(rew, np.float64),
+                        done=np.array(done, np.uint8), bodies=o.bodies())
+
+
 if __name__ == "__main__":
     spawn_fixture()
-    for e in range(5):
+    for e in range(7):
         trajectory(e)
     scenario_v0()
+    scenario_v3_heavy()
     print("golden fixtures written to", HERE)

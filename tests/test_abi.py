@@ -49,7 +49,8 @@ def test_python_binding_lists_every_symbol(lib):
 
 @pytest.mark.parametrize("env_id,dims", [
     (0, (28, 6, 7, 2, 1, 2000)), (1, (40, 15, 13, 5, 1, 3000)), (2, (39, 4, 7, 2, 1, 2000)),
-    (3, (39, 4, 7, 2, 1, 2000)), (4, (69, 4, 9, 2, 3, 2000))])
+    (3, (39, 4, 7, 2, 1, 2000)), (4, (69, 4, 9, 2, 3, 2000)), (5, (27, 6, 7, 2, 1, 1500)),
+    (6, (27, 6, 7, 2, 1, 1500))])
 def test_env_dims(lib, env_id, dims):
     from gym_puzzles_amd import env_dims
     d = env_dims(env_id)
@@ -58,7 +59,7 @@ def test_env_dims(lib, env_id, dims):
 
 def test_env_dims_match_oracle(lib, oracle_lib):
     from gym_puzzles_amd import env_dims
-    for e in range(5):
+    for e in range(7):
         d = env_dims(e)
         assert d["obs_dim"] == oracle_lib.or_obs_dim(e) and d["act_dim"] == oracle_lib.or_act_dim(e)
         assert d["n_draws"] == oracle_lib.or_n_draws(e)
@@ -74,8 +75,8 @@ def test_bad_env_id(lib):
 
 
 def test_state_words_positive(lib):
-    w = [lib.mrp_state_words(e) for e in range(5)]
-    assert all(x > 0 for x in w) and w[1] > w[0] and w[4] > w[2]
+    w = [lib.mrp_state_words(e) for e in range(7)]
+    assert all(x > 0 for x in w) and w[1] > w[0] and w[4] > w[2] and w[5] == w[6] == w[0]
     assert lib.mrp_state_words(11) < 0
 
 

@@ -91,9 +91,67 @@ def test_single_env_reference_test_flow(gpu_lib):
 
 
 @pytest.mark.gpu
+def test_v3_heavy_reference_test_flow(gpu_lib):
+    """gym_puzzles/tests/test_env.py itself: make('MultiRobotPuzzle-v3', heavy=True), seed 17,
+    obs = reset(), reset(), then action_space.sample() steps until done -- here the 1500-step
+    TimeLimit (tests/golden/scenario_v3heavy_seed17.npz)."""
+    import random
+
+    from gym_puzzles_amd import make
+    z = np.load(os.path.join(GOLDEN, "scenario_v3heavy_seed17.npz"))
+    np.random.seed(0)
+    env = make("MultiRobotPuzzle-v3", heavy=True)
+    assert env.unwrapped.env_id == 6 and env.observation_space.shape == (27,) and env.action_space.shape == (6,)
+    assert env.observation_space.high[2] == np.float32(2 * np.pi) and env.observation_space.low[-1] == -1.5
+    random.seed(17)
+    np.random.seed(17)
+    assert env.seed(17) == [17]
+    env.action_space.seed(17)
+    assert np.array_equal(env.reset().astype(np.float32), z["obs0"][0])
+    done = False
+    assert np.array_equal(env.reset().astype(np.float32), z["obs0"][1])
+    t = 0
+    while not done:
+        a = env.action_space.sample()
+        assert np.array_equal(a, z["acts"][t])
+        obs, rew, done, info = env.step(a)
+        assert np.array_equal(obs.astype(np.float32), z["obs"][t]), t
+        assert rew == pytest.approx(z["reward"][t], rel=1e-12, abs=1e-12) and np.float32(rew) == np.float32(z["reward"][t])
+        t += 1
+    assert t == z["acts"].shape[0] == 1500 and info == {"TimeLimit.truncated": True}
+    assert np.array_equal(env.unwrapped.bodies().ravel(), z["bodies"])
+    assert env.get_deltaBlk() == 50 and env.get_agentDist() == 0.1
+    env.close()
+
+
+@pytest.mark.gpu
+def test_v3_set_reward_params_and_completion_bonus(gpu_lib, oracle_lib):
+    """set_reward_params(puzzleComp=...) is the bonus step() adds (core.py:408-410); a block
+    spawned on the goal completes on the reset step and on the first step."""
+    from gym_puzzles_amd import Batch
+    from oracle import oracle
+    b = Batch(5, 2)
+    b.set_reward_params(10, 0.1, 50, 0.025, 7.0)
+    gx = 5 / 6 * 640 / 30 - 4 / 3 / 30
+    draws = np.array([[gx, 8.0, 0.3, 2.0, 2.0, 3.0, 12.0], [10.0, 8.0, 1.0, 2.0, 2.0, 3.0, 12.0]])
+    acts = np.zeros((2, 6), np.float32)
+    b.reset(draws, acts)
+    obs, rew, done, _ = b.step(acts)
+    o = [oracle.OracleEnv(5) for _ in range(2)]
+    for l in range(2):
+        o[l].reset(draws[l], acts[l])
+        ob, r, d, k = o[l].step(acts[l])
+        assert np.array_equal(obs[l], ob.astype(np.float32)) and int(d) == int(done[l])
+    assert done[0] == 1 and done[1] == 0 and b.status[0] == 1
+    assert b.reward64[0] > 6.0    # the 7.0 bonus, not the oracle's default 100 nor v0's 10000
+    b.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name,obs_dim,act_dim", [("MultiRobotPuzzleHeavy-v0", 40, 15), ("MultiRobotPuzzle-v2", 39, 4),
                                                   ("MultiRobotPuzzleHeavy-v2", 39, 4),
-                                                  ("MultiRobotPuzzleHeavy-v2-3block", 69, 4)])
+                                                  ("MultiRobotPuzzleHeavy-v2-3block", 69, 4),
+                                                  ("MultiRobotPuzzle-v3", 27, 6)])
 def test_single_env_spaces_and_step(gpu_lib, name, obs_dim, act_dim):
     from gym_puzzles_amd import make
     env = make(name)

@@ -17,7 +17,7 @@ from gym_puzzles_amd.spawn import draw_bounds, reference_draws
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-ENVS = range(5)
+ENVS = range(7)
 
 
 @pytest.fixture(scope="module")

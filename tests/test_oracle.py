@@ -6,7 +6,8 @@
 * closed-form free-flight kinematics of a v0 agent (velocity set, damping, integration;
   multi_robot_puzzle_00.py:415-424 + Box2D b2Island::Solve), float32 bit for bit;
 * a numpy restatement of the v0 observation/reward (multi_robot_puzzle_00.py:130-132,
-  277-291,430-521) recomputed from the oracle's body state;
+  277-291,430-521) and of the v3 observation/reward (core.py:65-67,289-350,369-414)
+  recomputed from the oracle's body state;
 * the committed golden fixtures (tests/golden/, see make_golden.py).
 Parity of the oracle against pybox2d itself is unpinned (no box2d-py here).
 """
@@ -64,6 +65,11 @@ AGENT_V2 = [(-0.039, -0.095), (0.039, -0.095), (0.095, -0.039), (0.095, 0.039), 
 
 
 def _expected_masses(env_id):
+    if env_id in (5, 6):   # Block("T") blocks.py:80-90 at scale 0.5 / 1, density 5 / 10; Robot robot.py:34-40
+        s, dens = (1.0, 10.0) if env_id == 6 else (0.5, 5.0)
+        blk = _compound([_poly_mass(_box(1 * s, 1 * s, 0, -1 * s), dens), _poly_mass(_box(3 * s, 1 * s, 0, 1 * s), dens)])
+        agent = _poly_mass([(x * 8.0, y * 8.0) for x, y in AGENT_V2], 5.0)
+        return [blk, agent, agent]
     if env_id in (0, 1):
         s = 2.0 if env_id == 1 else 1.0
         blk = _compound([_poly_mass(_box(0.5 * s, 0.5 * s, 0, -0.5 * s), 5.0 * (2 if env_id == 1 else 1)),
@@ -80,7 +86,7 @@ def _expected_masses(env_id):
     return [t, l_blk, i_blk, agent, agent]
 
 
-@pytest.mark.parametrize("env_id", range(5))
+@pytest.mark.parametrize("env_id", range(7))
 def test_mass_known_answers(orc, env_id):
     e = orc.OracleEnv(env_id)
     e.reset(reference_draws(env_id, np.random.RandomState(17)), np.zeros(e.act_dim, np.float32))
@@ -183,11 +189,76 @@ def test_v0_obs_and_reward_restatement(orc):
         prev_bd, prev_ad = bd, ad
 
 
+def _t_vertices_v3(s):
+    wide = [(-3 * s, 0.0), (3 * s, 0.0), (3 * s, 2 * s), (-3 * s, 2 * s)]   # box(3s, s) at (0, s), newest first
+    stem = [(-s, -2 * s), (s, -2 * s), (s, 0.0), (-s, 0.0)]
+    return np.array(wide + stem, np.float64)
+
+
+@pytest.mark.parametrize("env_id", [5, 6])
+def test_v3_obs_and_reward_restatement(orc, env_id):
+    """Recompute the v3 observation and reward in numpy from the oracle's bodies: normalised
+    poses (x - ws) / ws, (y - hs) / ws, angle % 2 pi; the goal (5/6 * 640 - 4/3, 240) px; eight
+    normalised T vertices; reward weights 50 / 0.025 / 10 / 0.1 with the agent terms over 4."""
+    ws, hs = 640 / 30 / 2, 480 / 30 / 2
+    gx, gy = (5 / 6 * 640 - 4 / 3 - 320) / 320, (240 - 240) / 320
+    s = 1.0 if env_id == 6 else 0.5
+    e = orc.OracleEnv(env_id)
+    rs = np.random.RandomState(8)
+    obs = e.reset(reference_draws(env_id, rs), rs.uniform(-1, 1, 6).astype(np.float32))
+    verts = _t_vertices_v3(s)
+    lcy = e.body_mass(0)[3]
+
+    def poses(b):
+        n = lambda x, y: ((x - ws) / ws, (y - hs) / ws)
+        return n(*b[0, :2].astype(np.float64)), [n(*b[1 + i, :2].astype(np.float64)) for i in range(2)]
+
+    def dists(b):
+        (bx, by), ag = poses(b)
+        return math.hypot(bx - gx, by - gy), [math.hypot(ax - bx, ay - by) for ax, ay in ag]
+
+    prev_bd, prev_ad = dists(e.bodies().reshape(3, 6))
+    for t in range(60):
+        a = rs.uniform(-1, 1, 6).astype(np.float32)
+        obs, rew, done, _ = e.step(a)
+        b = e.bodies().reshape(3, 6)
+        (bx, by), ag = poses(b)
+        bd, ad = dists(b)
+        brot = float(b[0, 2]) % (2 * np.pi)
+        exp = []
+        for i in range(2):
+            exp += [bx - ag[i][0], by - ag[i][1], float(b[1 + i, 2]) % (2 * np.pi), 0.0]
+        exp += [gx - bx, gy - by, 0.0 - brot]
+        ca, sa = math.cos(b[0, 2]), math.sin(b[0, 2])
+        ox, oy = b[0, 0] - (-sa * lcy), b[0, 1] - (ca * lcy)      # body origin from worldCenter
+        for vx, vy in verts:
+            exp += [(ox + ca * vx - sa * vy - ws) / ws, (oy + sa * vx + ca * vy - hs) / ws]
+        np.testing.assert_allclose(obs, exp, rtol=1e-5, atol=2e-5)
+        r = (prev_bd - bd) * 50 - 0.025 * bd
+        for i in range(2):
+            r += (prev_ad[i] - ad[i]) * 10 / 4. - 0.1 * ad[i] / 4.
+        if bd <= 25 / 640 * 2:
+            r += 100
+        assert rew == pytest.approx(r, rel=1e-5, abs=1e-5)
+        assert bool(done) == (bd <= 25 / 640 * 2)
+        assert e.flags()[0].tolist() == [0, 0]   # the v3 contact detector never fires
+        prev_bd, prev_ad = bd, ad
+
+
+def test_v3_draw_bounds_match_reference_ranges():
+    """core.py:212-215 (block x, y, angle) and :231-232 (agent x, y), BORDER = 1, SCALE = 30."""
+    for env_id in (5, 6):
+        b = draw_bounds(env_id)
+        assert b[0] == pytest.approx((640 / 30 / 3 + 2, 640 / 30 * 2 / 3 - 2)) and b[1] == (3, 480 / 30 - 3)
+        assert b[2] == (0, 2 * np.pi) and b[3] == pytest.approx((1, 640 / 30 / 3 - 2)) and b[4] == (1, 480 / 30 - 1)
+        assert len(b) == 7
+
+
 # ----------------------------------------------------------------------------- golden fixtures
 def test_spawn_draw_golden():
     with open(os.path.join(GOLDEN, "spawn_draws.json")) as f:
         g = json.load(f)
-    for env_id in range(5):
+    for env_id in range(7):
         for seed in (0, 17, 2021):
             np.random.seed(seed)
             assert np.array_equal(reference_draws(env_id), np.array(g[f"draws/{env_id}/{seed}"]))
@@ -222,7 +293,7 @@ def _replay_golden(orc, env_id):
                 assert np.array_equal(o.reset(z["rdraws"][t, l], z["racts"][t, l]).astype(np.float32), z["robs"][t, l])
 
 
-@pytest.mark.parametrize("env_id", range(5))
+@pytest.mark.parametrize("env_id", range(7))
 def test_oracle_matches_golden_trajectory(orc, env_id):
     _replay_golden(orc, env_id)
 

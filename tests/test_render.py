@@ -12,7 +12,7 @@ import pytest
 
 from oracle import render_ref
 
-ENVS = range(5)
+ENVS = range(7)
 
 
 def _dims(env_id):
@@ -62,7 +62,8 @@ def test_render_parity(gpu_lib, env_id):
     from gym_puzzles_amd import Batch
     from gym_puzzles_amd._native import shapes
     b = Batch(env_id, 4, seed=123)
-    if env_id >= 2:
+    v2 = 2 <= env_id <= 4
+    if v2:
         b.update_params(0, 1.0)
         b.update_goal(0, 1)   # scaled_epsilon = 0.1 * 2
     b.reset()
@@ -71,8 +72,8 @@ def test_render_parity(gpu_lib, env_id):
     d = _dims(env_id)
     nd = d["n_agents"] + d["n_blocks"]
     state, goals, sh = b.get_state(), b.get_goals(), shapes(env_id)
-    eps = 0.2 if env_id >= 2 else 25.0
-    for (w, h) in ((None, None), (160 if env_id <= 1 else 360, 120 if env_id <= 1 else 202)):
+    eps = 0.2 if v2 else 25.0
+    for (w, h) in ((None, None), (360 if v2 else 160, 202 if v2 else 120)):
         frames = b.render([0, 3, 1], width=w, height=h)
         W, H = frames.shape[2], frames.shape[1]
         for k, lane in enumerate([0, 3, 1]):
@@ -82,6 +83,27 @@ def test_render_parity(gpu_lib, env_id):
             bad = np.argwhere((frames[k] != ref).any(axis=2))
             assert len(bad) == 0, f"lane {lane} {W}x{H}: {len(bad)} pixels differ, first {bad[0]}"
         assert (frames[0] != 0).any()
+
+
+def test_oracle_scene_v3_hand_placed():
+    """A v3 lane: four wall polygons (no boundary polyline), Block.draw and Robot.draw at the v0
+    sizes, the goal disc at (532, 240) px drawn last (core.py:421-459)."""
+    from gym_puzzles_amd._native import shapes
+    sh = shapes(5)
+    xf = np.array([[10.0, 8.0, 0.0, 1.0], [4.0, 4.0, 0.0, 1.0], [5.0, 12.0, 0.0, 1.0]], np.float32)
+    centers = np.array([[10.0, 8.25], [4.0, 4.0], [5.0, 12.0]], np.float32)
+    goals = np.array([[5 / 6 * 640 - 4 / 3, 240.0, 0.0]])
+    prims = render_ref.build_scene(5, sh, 2, 1, xf, centers, goals)
+    img = render_ref.rasterise(5, prims, 640, 480)
+    px = lambda x, y: tuple(img[479 - int(y * 30), int(x * 30)])
+    assert px(1.5, 8.0) == (0, 0, 0)              # no boundary polyline at BORDER = 1 m
+    assert px(0.2, 8.0) == (51, 51, 51)           # left wall polygon
+    assert px(10.0, 7.6) == (128, 128, 128)       # T block stem (half-width 0.5 at scale 0.5)
+    assert px(10.0, 8.25) == (255, 255, 255)      # block centroid disc
+    assert px(4.5, 4.0) == (255, 255, 255)        # robot hull (0.76 m across)
+    assert px(4.0, 4.0) == (128, 128, 128)        # robot centre disc
+    assert px(532 / 30, 8.0) == (58, 153, 255)    # goal disc
+    assert len(prims) == 4 + 2 + 1 + 8 + 2 * 2 + 1
 
 
 @pytest.mark.gpu
