@@ -20,6 +20,8 @@
  *          2 MultiRobotPuzzle-v2       (gym_puzzles/__init__.py:17-22, multi_robot_puzzle_02.py:126)
  *          3 MultiRobotPuzzleHeavy-v2  (gym_puzzles/__init__.py:24-29, multi_robot_puzzle_02.py:711)
  *          4 MultiRobotPuzzleHeavy-v2 with the build-defined 3-block square
+ *          5 MultiRobotPuzzle-v3       (gym_puzzles/__init__.py:31-35, core.py:77 RobotPuzzleBase)
+ *          6 MultiRobotPuzzle-v3 constructed with heavy=True (gym_puzzles/tests/test_env.py:12)
  */
 #ifndef MRP_H
 #define MRP_H
@@ -65,10 +67,12 @@ int mrp_env_id(const mrp_ctx* ctx);
 int mrp_set_stream(mrp_ctx* ctx, void* hip_stream);
 int mrp_synchronize(mrp_ctx* ctx);
 
-/* set_reward_params (multi_robot_puzzle_00.py:231-239, _02.py:216-225). */
+/* set_reward_params (multi_robot_puzzle_00.py:231-239, _02.py:216-225; v3 core.py:149-155, where
+ * puzzle_comp is the completion bonus step() adds unshaped and the two penalties are unused). */
 int mrp_set_reward_params(mrp_ctx* ctx, double agent_delta, double agent_distance, double block_delta,
                           double block_distance, double puzzle_comp, double out_of_bounds, double blk_out_of_bounds);
-/* update_params(timestep, decay) (multi_robot_puzzle_00.py:241-243, _02.py:227-230). */
+/* update_params(timestep, decay) (multi_robot_puzzle_00.py:241-243, _02.py:227-230; v3 stores a value
+ * its step() never reads, core.py:158-159, so it changes nothing there). */
 int mrp_update_params(mrp_ctx* ctx, double timestep, double decay);
 /* update_goal(epoch, nb_epochs) (multi_robot_puzzle_00.py:245-246, _02.py:232-233). */
 int mrp_update_goal(mrp_ctx* ctx, double epoch, double nb_epochs);
