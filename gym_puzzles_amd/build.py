@@ -3,24 +3,31 @@
 Numerics flags are part of the contract: -ffp-contract=off (no FMA contraction, so float32
 expressions round exactly like the box2d-py engine), no fast-math, f32 denormals kept,
 correctly rounded f32 divide/sqrt.
+
+Each env id's lane kernels are their own translation unit (csrc/mrp_env<E>.hip), so the units
+compile in parallel and are linked into one shared library.
 """
 from __future__ import annotations
 
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmrp.so")
-SOURCES = [os.path.join(CSRC, "mrp_kernels.hip"), os.path.join(CSRC, "mrp_tables.cpp"), os.path.join(CSRC, "mrp_norm.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("mrp_math.h", "mrp_config.h", "mrp_world.h", "mrp_env.h", "mrp_tables.h")] + [
+N_ENVS = 7
+SOURCES = ([os.path.join(CSRC, "mrp_kernels.hip"), os.path.join(CSRC, "mrp_tables.cpp"), os.path.join(CSRC, "mrp_norm.hip")]
+           + [os.path.join(CSRC, f"mrp_env{e}.hip") for e in range(N_ENVS)])
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("mrp_math.h", "mrp_config.h", "mrp_world.h", "mrp_env.h", "mrp_tables.h",
+                                                  "mrp_ops.h", "mrp_lane.h", "mrp_render.h")] + [
     os.path.join(HERE, "..", "include", "mrp.h")]
 # -fno-slp-vectorize: the serial solver chains are latency-bound; packing pairs of f32 ops into
 # v_pk_* costs operand-shuffling moves on the dependency chain (measured +2-3 % env-steps/s off)
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
          "-fno-gpu-flush-denormals-to-zero", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-strict-aliasing",
-         "-fno-slp-vectorize", "-fPIC", "-shared"]
+         "-fno-slp-vectorize", "-fPIC"]
 
 
 def hipcc() -> str:
@@ -37,11 +44,27 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(d) <= t for d in DEPS if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
+def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=(), jobs: int | None = None) -> str:
     """Build libmrp.so (or a diagnostic variant with extra -D defines into ``out``)."""
     if not force and out == OUT and up_to_date():
         return out
-    cmd = [hipcc()] + FLAGS + [f"-D{d}" for d in defines] + SOURCES + ["-o", out + ".tmp"]
+    objdir = os.path.join(HERE, "build", os.path.basename(out) + ".obj")
+    os.makedirs(objdir, exist_ok=True)
+    dflags = [f"-D{d}" for d in defines]
+    objs = [os.path.join(objdir, os.path.basename(s) + ".o") for s in SOURCES]
+
+    def compile_one(i: int) -> None:
+        cmd = [hipcc()] + FLAGS + dflags + ["-c", SOURCES[i], "-o", objs[i]]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+
+    # slowest units first; each hipcc is single-threaded, so one job per core
+    jobs = jobs or max(1, min(len(SOURCES), os.cpu_count() or 1, int(os.environ.get("MAX_JOBS", "16"))))
+    order = sorted(range(len(SOURCES)), key=lambda i: "mrp_env" not in SOURCES[i])
+    with ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(compile_one, order))
+    cmd = [hipcc()] + FLAGS + ["-shared"] + objs + ["-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -1,0 +1,357 @@
+// mrp_lane.h -- the lane kernels of one env id, included once per translation unit by
+// mrp_env<E>.hip with MRP_ENV set (build.py compiles the seven units in parallel).
+//
+// Execution model: one wavefront (64 threads, one workgroup) owns one world ("lane").  The
+// lane's persistent state is contiguous in HBM (lane-major, so the wave moves it with
+// coalesced 16-B loads/stores) and lives in LDS for the whole step; order-sensitive Box2D
+// work (tree updates, contact-list edits, events, island set-up) runs on thread 0, while
+// the data-parallel phases (SAT narrow phase of every contact, broad-phase pair tests, TOI of
+// every candidate contact, the island solver sweeps, state/obs I/O) are spread over the 64
+// threads.  There is no dense contraction in this path, so no MFMA: the work is fp32 VALU with
+// data-dependent control flow, plus fp64 for the env-level arithmetic.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstring>
+
+#include "mrp_env.h"
+#include "mrp_ops.h"
+
+#ifndef MRP_ENV
+#error "define MRP_ENV (the env id this translation unit instantiates)"
+#endif
+
+using namespace mrp;
+
+// this unit's copy of the env tables (uploaded by EnvOps::upload_tables at mrp_create)
+static __constant__ EnvTables g_tables[N_ENVS];
+
+#include "mrp_render.h"
+
+namespace {
+// LaneState is copied word-by-word; a may_alias word type keeps type-based alias analysis
+// from reordering these copies against the typed (float/int) accesses of the step code.
+typedef uint32_t __attribute__((__may_alias__)) word_t;
+
+template <int ENV>
+__device__ __forceinline__ void load_state(LaneState<ENV>& S, const uint32_t* __restrict__ g, int lane, int tid) {
+    static_assert(sizeof(LaneState<ENV>) % 16 == 0, "lane state moves in 16-B granules");
+    constexpr int NQ = (int)(sizeof(LaneState<ENV>) / 16);
+    typedef uint4 __attribute__((__may_alias__)) quad_t;
+    quad_t* w = reinterpret_cast<quad_t*>(&S);
+    const quad_t* src = reinterpret_cast<const quad_t*>(g + (size_t)lane * lane_words<ENV>());
+    for (int i = tid; i < NQ; i += BLOCK) w[i] = src[i];
+}
+template <int ENV>
+__device__ __forceinline__ void store_state(const LaneState<ENV>& S, uint32_t* __restrict__ g, int lane, int tid) {
+    constexpr int NQ = (int)(sizeof(LaneState<ENV>) / 16);
+    typedef uint4 __attribute__((__may_alias__)) quad_t;
+    const quad_t* w = reinterpret_cast<const quad_t*>(&S);
+    quad_t* dst = reinterpret_cast<quad_t*>(g + (size_t)lane * lane_words<ENV>());
+    for (int i = tid; i < NQ; i += BLOCK) dst[i] = w[i];
+}
+
+// copy this env's hot tables from __constant__ memory into the lane's LDS (before the
+// barrier that follows load_state)
+template <int ENV>
+__device__ __forceinline__ void load_tables(LdsTables<ENV>& L, int tid) {
+    using LT = LdsTables<ENV>;
+    const EnvTables& T = g_tables[ENV];
+    constexpr int SW = LT::NF * (int)(sizeof(ShapeDef) / 4);
+    const word_t* src = reinterpret_cast<const word_t*>(T.shape);
+    word_t* dst = reinterpret_cast<word_t*>(L.shape);
+    for (int i = tid; i < SW; i += BLOCK) dst[i] = src[i];
+    if (tid < LT::NF) {
+        L.fix_body[tid] = T.fix_body[tid]; L.fix_friction[tid] = T.fix_friction[tid];
+        L.fix_restitution[tid] = T.fix_restitution[tid];
+    }
+    if (tid < LT::NBODY) {
+        L.invMass[tid] = T.invMass[tid]; L.invI[tid] = T.invI[tid]; L.lcx[tid] = T.lcx[tid]; L.lcy[tid] = T.lcy[tid];
+        L.linDamp[tid] = T.linDamp[tid]; L.angDamp[tid] = T.angDamp[tid];
+        L.body_fix0[tid] = T.body_fix0[tid]; L.body_nfix[tid] = T.body_nfix[tid];
+    }
+    if (tid < 4) { L.wall_px[tid] = T.wall_px[tid]; L.wall_py[tid] = T.wall_py[tid]; }
+}
+
+template <int ENV>
+__global__ __launch_bounds__(BLOCK) void k_init(uint32_t* state, int nl) {
+    __shared__ Shared<ENV> sh;
+    const int lane = blockIdx.x, tid = threadIdx.x;
+    if (lane >= nl) return;
+    word_t* w = reinterpret_cast<word_t*>(&sh.S);
+    for (int i = tid; i < lane_words<ENV>(); i += BLOCK) w[i] = 0;
+    __syncthreads();
+    if (tid == 0) {
+        EnvParams P;
+        memset(&P, 0, sizeof(P));
+        Env<ENV> e(sh, g_tables[ENV], P, 0);
+        e.init_empty_world();
+    }
+    __syncthreads();
+    store_state<ENV>(sh.S, state, lane, tid);
+}
+
+// stage one reset's draws/action into LDS: host-provided rows or the counter RNG
+template <int ENV>
+__device__ void stage_reset_inputs(Shared<ENV>& sh, const double* draws, const float* actions, int lane, int tid,
+                                   uint64_t seed, uint64_t glane) {
+    using D = Dims<ENV>;
+    const EnvTables& T = g_tables[ENV];
+    const uint64_t ctr = (uint64_t)(uint32_t)sh.S.episode * 64u;
+    if (tid < D::NDRAW)
+        sh.draws[tid] = draws ? draws[(size_t)lane * D::NDRAW + tid]
+                              : T.draw_lo[tid] + (T.draw_hi[tid] - T.draw_lo[tid]) * rng_u01(seed, glane, 1, ctr + tid);
+    if (tid < D::ACT)
+        sh.act[tid] = actions ? actions[(size_t)lane * D::ACT + tid] : (float)(-1.0 + 2.0 * rng_u01(seed, glane, 2, ctr + tid));
+    __syncthreads();
+    if (tid == 0) { sh.S.episode += 1; sh.S.elapsed = 0; }
+    __syncthreads();
+}
+
+template <int ENV>
+__global__ __launch_bounds__(BLOCK, 4) void k_reset(uint32_t* state, int nl, const uint8_t* mask, const double* draws,
+                                                 const float* actions, float* obs, EnvParams P, uint64_t seed,
+                                                 uint64_t lane_offset) {
+    using D = Dims<ENV>;
+    __shared__ Shared<ENV> sh;
+    const int lane = blockIdx.x, tid = threadIdx.x;
+    if (lane >= nl) return;
+    if (mask && !mask[lane]) return;
+    load_state<ENV>(sh.S, state, lane, tid);
+    load_tables<ENV>(sh.lt, tid);
+    __syncthreads();
+    stage_reset_inputs<ENV>(sh, draws, actions, lane, tid, seed, lane_offset + lane);
+    Env<ENV> e(sh, g_tables[ENV], P, tid);
+    e.env_reset_coop();
+    for (int k = tid; k < D::OBS; k += BLOCK) obs[(size_t)lane * D::OBS + k] = sh.obs[k];
+    store_state<ENV>(sh.S, state, lane, tid);
+}
+
+template <int ENV>
+__global__ __launch_bounds__(BLOCK, 4) void k_step(uint32_t* state, int nl, const float* actions, float* obs, float* reward,
+                                                double* reward64, uint8_t* done_out, uint8_t* trunc_out, uint8_t* status_out, float* term_obs,
+                                                EnvParams P, uint64_t seed, uint64_t lane_offset, int auto_reset,
+                                                int max_steps, const int* __restrict__ order, uint32_t* __restrict__ cost,
+                                                const uint32_t* __restrict__ costmax) {
+    using D = Dims<ENV>;
+    __shared__ Shared<ENV> sh;
+    __shared__ int s_fin;
+    const int tid = threadIdx.x;
+    if ((int)blockIdx.x >= nl) return;
+    // workgroup b steps lane order[b]: the previous step's costliest lanes are dispatched first
+    // (k_order), so no SIMD collects several long serial chains; a lane's result does not depend
+    // on which workgroup steps it
+    const int lane = order ? order[blockIdx.x] : (int)blockIdx.x;
+    const unsigned long long t_start = cost ? __builtin_amdgcn_s_memtime() : 0ull;
+    const uint64_t glane = lane_offset + lane;
+#ifdef MRP_STAMPS
+    if (tid == 0) { sh.stamp_t = sh.stamp_t0 = __builtin_amdgcn_s_memtime(); sh.stamp_rt0 = __builtin_amdgcn_s_memrealtime(); }
+    if (tid < 16) sh.trace[tid] = 0;
+    long long toi0 = 0, pos0 = 0;
+#endif
+    load_state<ENV>(sh.S, state, lane, tid);
+    load_tables<ENV>(sh.lt, tid);
+    __syncthreads();
+#ifdef MRP_STAMPS
+    toi0 = sh.S.toiEvents; pos0 = sh.S.posIters;
+#endif
+    MRP_STAMP(0);
+    const uint64_t ctr = (uint64_t)sh.S.stepCounter * 64u;
+    if (tid < D::ACT)
+        sh.act[tid] = actions ? actions[(size_t)lane * D::ACT + tid] : (float)(-1.0 + 2.0 * rng_u01(seed, glane, 3, ctr + tid));
+    __syncthreads();
+    if (tid == 0) sh.S.stepCounter += 1;
+    Env<ENV> e(sh, g_tables[ENV], P, tid);
+    if (costmax) {   // priority from the lane's previous-step cost relative to the slowest lane's
+        const uint64_t c = cost[lane], m = *costmax;
+        e.prio_floor = __builtin_amdgcn_readfirstlane(4 * c > 3 * m ? 3 : (2 * c > m ? 2 : (4 * c > m ? 1 : 0)));
+        e.set_prio(e.prio_floor);
+    }
+    e.env_step_coop();
+    if (tid == 0) {
+        sh.S.elapsed += 1;
+        int d = sh.done, tr = 0;
+        if (max_steps > 0 && sh.S.elapsed >= max_steps) { tr = !d; d = 1; }   // gym TimeLimit
+        if (reward) reward[lane] = (float)sh.reward;
+        if (reward64) reward64[lane] = sh.reward;   // the reference's Python float
+        if (done_out) done_out[lane] = (uint8_t)d;
+        if (trunc_out) trunc_out[lane] = (uint8_t)tr;
+        if (status_out) status_out[lane] = (uint8_t)sh.kind;
+        s_fin = d;
+    }
+    __syncthreads();
+    float* orow = obs + (size_t)lane * D::OBS;
+    if (term_obs)
+        for (int k = tid; k < D::OBS; k += BLOCK) term_obs[(size_t)lane * D::OBS + k] = sh.obs[k];
+    MRP_STAMP(8);
+    if (s_fin && auto_reset) {   // SB3-style auto-reset with device-RNG spawns
+        stage_reset_inputs<ENV>(sh, nullptr, nullptr, lane, tid, seed, glane);
+        e.env_reset_coop();
+        MRP_STAMP(9);
+    }
+    for (int k = tid; k < D::OBS; k += BLOCK) orow[k] = sh.obs[k];
+    store_state<ENV>(sh.S, state, lane, tid);
+    if (cost && tid == 0) cost[lane] = (uint32_t)min(__builtin_amdgcn_s_memtime() - t_start, 0xffffffffull);
+    MRP_STAMP(10);
+#ifdef MRP_STAMPS
+    if (tid == 0) {
+        unsigned long long tot = sh.stamp_t - sh.stamp_t0;
+        for (int k = 0; k < 11; ++k) { atomicAdd(&g_stamps[k], (unsigned long long)sh.trace[k]); atomicMax(&g_pmax[k], (unsigned long long)sh.trace[k]); }
+        atomicAdd(&g_rt[0], tot);
+        atomicAdd(&g_rt[1], __builtin_amdgcn_s_memrealtime() - sh.stamp_rt0);
+        atomicMax(&g_stepmax[(sh.S.stepCounter - 1u) & 255u], tot);
+        sh.trace[11] = (uint32_t)tot;
+        sh.trace[13] = (uint32_t)(sh.S.toiEvents - toi0);
+        sh.trace[14] = (uint32_t)(sh.S.posIters - pos0);
+    }
+    __syncthreads();
+    if (tid < 16 && lane < 16384) g_trace[lane][tid] = sh.trace[tid];
+#endif
+}
+
+template <int ENV>
+__global__ __launch_bounds__(BLOCK) void k_bodies(const uint32_t* state, int nl, float* out, int32_t* flags) {
+    using D = Dims<ENV>;
+    const int lane = blockIdx.x, tid = threadIdx.x;
+    if (lane >= nl || tid != 0) return;
+    const LaneState<ENV>& S = *reinterpret_cast<const LaneState<ENV>*>(state + (size_t)lane * lane_words<ENV>());
+    constexpr int ND = D::NA + D::NB;
+    if (out) {
+        float* r = out + (size_t)lane * 6 * ND;
+        for (int b = 0; b < ND; ++b) {
+            r[6 * b] = S.cx[b]; r[6 * b + 1] = S.cy[b]; r[6 * b + 2] = S.a[b];
+            r[6 * b + 3] = S.vx[b]; r[6 * b + 4] = S.vy[b]; r[6 * b + 5] = S.w[b];
+        }
+    }
+    if (flags) {
+        int32_t* f = flags + (size_t)lane * (D::NA + 1);
+        for (int i = 0; i < D::NA; ++i) f[i] = S.goal_contact[i];
+        f[D::NA] = S.blks_in_place;
+    }
+}
+
+template <int ENV>
+__global__ __launch_bounds__(256) void k_faults(const uint32_t* state, int nl, int32_t* out) {
+    const int lane = blockIdx.x * 256 + threadIdx.x;
+    if (lane >= nl) return;
+    const LaneState<ENV>& S = *reinterpret_cast<const LaneState<ENV>*>(state + (size_t)lane * lane_words<ENV>());
+    out[lane] = S.fault;
+}
+
+// ------------------------------------------------------------------------------ launch table
+template <int ENV>
+struct Launch {
+    static hipError_t upload_tables(const EnvTables* all) {
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_tables), all, sizeof(EnvTables) * N_ENVS);
+    }
+    static void init(hipStream_t s, uint32_t* state, int nl) {
+        hipLaunchKernelGGL(k_init<ENV>, dim3(nl), dim3(BLOCK), 0, s, state, nl);
+    }
+    static void reset(hipStream_t s, uint32_t* state, int nl, const uint8_t* mask, const double* draws, const float* actions,
+                      float* obs, const EnvParams& P, uint64_t seed, uint64_t lane_offset) {
+        hipLaunchKernelGGL(k_reset<ENV>, dim3(nl), dim3(BLOCK), 0, s, state, nl, mask, draws, actions, obs, P, seed, lane_offset);
+    }
+    static void step(hipStream_t s, const StepArgs& a) {
+        hipLaunchKernelGGL(k_step<ENV>, dim3(a.nl), dim3(BLOCK), 0, s, a.state, a.nl, a.actions, a.obs, a.reward, a.reward64,
+                           a.done, a.trunc, a.status, a.term_obs, a.P, a.seed, a.lane_offset, a.auto_reset, a.max_steps,
+                           a.order, a.cost, a.costmax);
+    }
+    static void bodies(hipStream_t s, const uint32_t* state, int nl, float* out, int32_t* flags) {
+        hipLaunchKernelGGL(k_bodies<ENV>, dim3(nl), dim3(BLOCK), 0, s, state, nl, out, flags);
+    }
+    static void faults(hipStream_t s, const uint32_t* state, int nl, int32_t* out) {
+        hipLaunchKernelGGL(k_faults<ENV>, dim3((nl + 255) / 256), dim3(256), 0, s, state, nl, out);
+    }
+    static void render(hipStream_t s, dim3 grid, const uint32_t* state, const int32_t* lanes, int nl, int W, int H,
+                       const mrpr::RenderArgs& A, uint8_t* rgb) {
+        hipLaunchKernelGGL(mrpr::k_render<ENV>, grid, dim3(mrpr::RBLOCK), 0, s, state, lanes, nl, W, H, A, rgb);
+    }
+    static void goals(hipStream_t s, const uint32_t* state, int nl, double* out) {
+        hipLaunchKernelGGL(mrpr::k_goals<ENV>, dim3((nl + 255) / 256), dim3(256), 0, s, state, nl, out);
+    }
+    static hipError_t debug_read(int what, void* out, size_t bytes) {
+#ifdef MRP_STAMPS
+        static char zero[16384 * 16 * 4];
+        hipError_t e = hipDeviceSynchronize();
+        const void* sym = what == DBG_STAMPS ? (const void*)HIP_SYMBOL(g_stamps) : what == DBG_PMAX ? (const void*)HIP_SYMBOL(g_pmax)
+                        : what == DBG_STEPMAX ? (const void*)HIP_SYMBOL(g_stepmax) : what == DBG_RT ? (const void*)HIP_SYMBOL(g_rt)
+                        : (const void*)HIP_SYMBOL(g_trace);
+        if (e == hipSuccess) e = hipMemcpyFromSymbol(out, sym, bytes);
+        if (e == hipSuccess && what != DBG_TRACE) e = hipMemcpyToSymbol(sym, zero, bytes);
+        return e;
+#else
+        (void)what; (void)out; (void)bytes;
+        return hipErrorNotSupported;
+#endif
+    }
+    static hipError_t debug_progress(uint32_t* dev_words) {
+#ifdef MRP_PROGRESS
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_progress), &dev_words, sizeof(dev_words));
+#else
+        (void)dev_words;
+        return hipErrorNotSupported;
+#endif
+    }
+    static constexpr EnvOps ops() {
+        return EnvOps{lane_words<ENV>(), (int)(offsetof(LaneState<ENV>, toiEvents) / 4), upload_tables, init, reset, step,
+                      bodies, faults, render, goals, debug_read, debug_progress};
+    }
+};
+
+}  // namespace
+
+// the table is host data: the device-side pass of the unit must not see its initializer, but
+// it must instantiate the kernels the launchers name
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MRP_DEFINE_ENV_OPS(E) namespace { template struct Launch<E>; }
+#else
+#define MRP_DEFINE_ENV_OPS(E) \
+    namespace mrp { extern const EnvOps g_env_ops_##E; const EnvOps g_env_ops_##E = Launch<E>::ops(); }
+#endif
+
+#if MRP_ENV == 0
+namespace {
+// Diagnostic micro-benchmark of the lane-distributed velocity sweeps (mrp_debug_velbench): a
+// synthetic v0 island of nc agent-block contacts with pcount manifold points each, swept `iters`
+// times with the early exit off; out[block] = s_memtime cycles of the sweeps.
+__global__ __launch_bounds__(BLOCK, 4) void k_velbench(int nc, int pcount, int iters, unsigned long long* out) {
+    using W = World<0>;
+    __shared__ Shared<0> sh;
+    const int tid = threadIdx.x;
+    EnvParams P{};
+    W w(sh, g_tables[0], P, tid);
+    auto& is = sh.isl;
+    if (tid == 0) {
+        is.nb = nc + 1; is.nc = nc;
+        for (int b = 0; b <= nc; ++b) { is.vvx[b] = 0.3f * b - 0.1f; is.vvy[b] = 0.2f - 0.05f * b; is.vw[b] = b == 0 ? 0.01f : 0.0f; }
+        for (int i = 0; i < nc; ++i) {
+            VC& vc = sh.u.sol.vcs[i];
+            const float ang = 0.7f * (float)i + 0.3f;
+            vc.nx = __cosf(ang); vc.ny = __sinf(ang);
+            vc.iaI = i + 1; vc.ibI = 0; vc.mA = 1.0f; vc.iA = 0.0f; vc.mB = 0.05f; vc.iB = 1.0f / 17.0833f; vc.friction = 0.44f;
+            vc.pointCount = pcount;
+            for (int j = 0; j < 2; ++j) {
+                vc.rAx[j] = 0.1f * j - 0.2f; vc.rAy[j] = 0.75f; vc.rBx[j] = 0.4f + 0.3f * j; vc.rBy[j] = -0.6f;
+                vc.ni[j] = 0.2f; vc.ti[j] = 0.01f; vc.vbias[j] = 0.0f; vc.nmass[j] = 0.9f; vc.tmass[j] = 0.8f;
+            }
+            vc.k0 = 1.2f; vc.k1 = 0.3f; vc.k3 = 1.1f; vc.nm0 = 0.9f; vc.nm1 = -0.2f; vc.nm3 = 0.95f;
+        }
+    }
+    __syncthreads();
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    int sw = nc == 1 ? w.solver_velocity_one(is, sh.u.sol.vcs, iters, false)
+                     : (nc == 2 ? w.solver_velocity_two(is, sh.u.sol.vcs, iters, false) : -1);
+    if (sw < 0) w.solver_velocity_lanes(is, sh.u.sol.vcs, iters, false);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (tid == 0) out[blockIdx.x] = t1 - t0 + (is.vvx[0] == 12345.0f ? 1ull : 0ull);
+}
+}  // namespace
+hipError_t mrp::velbench_launch(const EnvTables* all, int nc, int pcount, int iters, int blocks, unsigned long long* d_out) {
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_tables), all, sizeof(EnvTables) * N_ENVS);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_velbench, dim3(blocks), dim3(BLOCK), 0, nullptr, nc, pcount, iters, d_out);
+    return hipGetLastError();
+}
+#endif

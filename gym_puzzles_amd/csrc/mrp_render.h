@@ -1,5 +1,6 @@
 // mrp_render.h -- batched rgb_array rendering of lanes straight from the SoA lane state
-// (SURVEY.md section 8f-3).  Included by mrp_kernels.hip after g_tables is declared.
+// (SURVEY.md section 8f-3).  Included by mrp_lane.h after g_tables is declared
+// (RenderArgs, RBLOCK and RPPT live in mrp_ops.h).
 //
 // Replaces the pyglet/OpenGL `render(mode='rgb_array')` of the reference:
 //   v0 / Heavy-v0 : gym_puzzles/envs/multi_robot_puzzle_00.py:528-592
@@ -24,8 +25,6 @@ using namespace mrp;
 
 enum : int { P_POLY = 0, P_CIRCLE = 1, P_RING = 2, P_RECT = 3 };
 constexpr int MAXPRIM = 64;
-constexpr int RBLOCK = 256;
-constexpr int RPPT = 8;       // pixels per thread: one display-list build serves RBLOCK*RPPT pixels
 constexpr float BPAD = 1e-4f;   // >> f32 rounding of the exact tests at these coordinates (|x| < 22 m)
 
 struct Prim {
@@ -34,13 +33,6 @@ struct Prim {
     float a, b, c, d;          // circle: cx, cy, r^2 ; ring: cx, cy, rin^2, rout^2 ; rect: xlo, ylo, xhi, yhi
     float bx0, by0, bx1, by1;  // conservative bounding box (padded by BPAD): culls before the exact test
     float vx[MAX_POLY], vy[MAX_POLY];
-};
-
-struct RenderArgs {
-    float sx, sy;              // world units per pixel
-    float lw_unit;             // world units per viewport pixel (line widths)
-    float ring_r;              // v2: scaled_epsilon / RATIO
-    double goal_scale;         // lane goal units -> world metres
 };
 
 __device__ __forceinline__ uint32_t rgb8(int r, int g, int b) { return (uint32_t)r | ((uint32_t)g << 8) | ((uint32_t)b << 16); }

@@ -32,11 +32,11 @@ extern "C" __device__ int mrp_writelane(int val, int lane, int old) __asm("llvm.
 // every lane accumulates s_memtime deltas per phase in LDS and publishes them into g_stamps /
 // g_pmax once, at the end of its step (no global atomics inside the timed phases).
 #ifdef MRP_STAMPS
-__device__ unsigned long long g_stamps[16];     // per-phase sums over lane-steps
-__device__ unsigned long long g_pmax[16];       // per-phase max over lane-steps
-__device__ unsigned long long g_stepmax[256];   // per step (stepCounter mod 256): slowest lane's total
-__device__ unsigned long long g_rt[2];          // sums of lane totals: s_memtime ticks, s_memrealtime ticks
-__device__ uint32_t g_trace[16384][16];         // last step per lane: phases 0-10, total, nc, toi, pos, vel-units
+static __device__ unsigned long long g_stamps[16];     // per-phase sums over lane-steps
+static __device__ unsigned long long g_pmax[16];       // per-phase max over lane-steps
+static __device__ unsigned long long g_stepmax[256];   // per step (stepCounter mod 256): slowest lane's total
+static __device__ unsigned long long g_rt[2];          // sums of lane totals: s_memtime ticks, s_memrealtime ticks
+static __device__ uint32_t g_trace[16384][16];         // last step per lane: phases 0-10, total, nc, toi, pos, vel-units
 #define MRP_TRACE(k, v) do { if (tid == 0) sh.trace[k] += (v); } while (0)
 #define MRP_STAMP(k)                                                                        \
     do {                                                                                    \
@@ -54,7 +54,7 @@ __device__ uint32_t g_trace[16384][16];         // last step per lane: phases 0-
 // of every lane stores the last progress point it reached into host-mapped memory, which a host
 // watchdog reads while a launch is still running (tools/hang_probe.py).
 #ifdef MRP_PROGRESS
-__device__ uint32_t* g_progress;
+static __device__ uint32_t* g_progress;
 #define MRP_PROG(k)                                                                                          \
     do {                                                                                                     \
         if (threadIdx.x == 0 && g_progress)                                                                  \
