@@ -24,8 +24,9 @@ namespace {
 __global__ __launch_bounds__(256) void k_sincos(const float* x, float* s, float* c, int n) {
     int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    s[i] = g_sinf(x[i]);
-    c[i] = g_cosf(x[i]);
+    const Rot q = rot(x[i]);   // b2Rot::Set as the step evaluates it
+    s[i] = q.s;
+    c[i] = q.c;
 }
 
 // Dispatch order for the next step: lanes by descending cost of this step (counting sort over 64
@@ -501,10 +502,10 @@ int mrp_debug_stamps_ext(int device, uint64_t* pmax16, uint64_t* stepmax256, uin
     return rc;
 }
 
-// Diagnostic builds only: the last step's per-lane trace (n_lanes x 16 words, n_lanes <= 16384).
+// Diagnostic builds only: the last step's per-lane trace (n_lanes x 24 words, n_lanes <= 16384).
 int mrp_debug_trace(int device, uint32_t* out, int n_lanes) {
     if (!out || n_lanes <= 0 || n_lanes > 16384 || hipSetDevice(device) != hipSuccess) return MRP_E_ARG;
-    std::vector<uint32_t> tmp((size_t)n_lanes * 16);
+    std::vector<uint32_t> tmp((size_t)n_lanes * 24);
     std::memset(out, 0, tmp.size() * 4);
     for (int i = 0; i < N_ENVS; ++i) {   // only the unit that stepped has a non-zero trace
         hipError_t e = env_ops(i)->debug_read(DBG_TRACE, tmp.data(), tmp.size() * 4);

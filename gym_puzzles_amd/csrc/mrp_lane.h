@@ -147,7 +147,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_step(uint32_t* state, int nl, cons
     const uint64_t glane = lane_offset + lane;
 #ifdef MRP_STAMPS
     if (tid == 0) { sh.stamp_t = sh.stamp_t0 = __builtin_amdgcn_s_memtime(); sh.stamp_rt0 = __builtin_amdgcn_s_memrealtime(); }
-    if (tid < 16) sh.trace[tid] = 0;
+    if (tid < MRP_TRACE_W) sh.trace[tid] = 0;
     long long toi0 = 0, pos0 = 0;
 #endif
     load_state<ENV>(sh.S, state, lane, tid);
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_step(uint32_t* state, int nl, cons
         sh.trace[14] = (uint32_t)(sh.S.posIters - pos0);
     }
     __syncthreads();
-    if (tid < 16 && lane < 16384) g_trace[lane][tid] = sh.trace[tid];
+    if (tid < MRP_TRACE_W && lane < 16384) g_trace[lane][tid] = sh.trace[tid];
 #endif
 }
 

@@ -160,10 +160,46 @@ MRP_HD float g_cosf(float y) {
     return (y - y) / (y - y);
 }
 
+// b2Rot::Set for |angle| < 120 without branches: glibc's fast-reduction path evaluated for every
+// input below 120 (for |y| < pi/4 that path reduces with n = 0, xr = fma(-0.0, pi/2, x) = x, sign
+// +1, which is exactly glibc's small-argument branch), both polynomials always, the quadrant
+// picks and glibc's |y| < 2^-12 early returns as selects.  The same double operations in the same
+// order as g_sinf / g_cosf, so bit-identical to them; no scalar branch and no VALU -> SALU round
+// trip on the dependency chain (the branchy form took 430 cycles per call on one wave, serially
+// dependent calls; this form exists because the position passes call it once per contact point).
+MRP_HD Rot rot_fast(float y) {
+    const double x = y;
+    const double r = x * SC_HPI_INV;
+    const int n = ((int32_t)r + 0x800000) >> 24;
+    const double xr = fma(-(double)n, SC_HPI, x);
+    const double xs = ((n + 1) & 2) ? -xr : xr;   // x * sign[n & 3] (an exact negation)
+    const double x2 = xr * xr;                      // (x * s) * (x * s) == x * x
+    // sin polynomial of xs (glibc sinf_poly, even n)
+    const double x3 = xs * x2;
+    const double s1 = fma(x2, SC_S3, SC_S2);
+    const double x7 = x3 * x2;
+    const double ss = fma(x3, SC_S1, xs);
+    const float ps = (float)fma(x7, s1, ss);
+    // cos polynomial (odd n): depends on x2 only
+    const double x4 = x2 * x2;
+    const double c2 = fma(x2, SC_C4, SC_C3);
+    const double c1 = fma(x2, SC_C1, SC_C0);
+    const double x6 = x4 * x2;
+    const double cc = fma(x4, SC_C2, c1);
+    const float pc0 = (float)fma(x6, c2, cc);
+    const float pc = (n & 2) ? -pc0 : pc0;          // the negated second table
+    const bool odd = (n & 1) != 0;
+    const bool tiny = abstop12(y) < abstop12(0x1p-12f);
+    Rot q;
+    q.s = tiny ? y : (odd ? pc : ps);
+    q.c = tiny ? 1.0f : (odd ? ps : pc);
+    return q;
+}
+
 // b2Rot::Set(angle) = {sinf(angle), cosf(angle)}: g_sinf and g_cosf fused over one range
 // reduction (the reduction and the sign pick are the same function of the input in both, so
 // each result is bit-identical to its standalone routine).
-MRP_HD Rot rot(float y) {
+MRP_HD Rot rot_slow(float y) {
     Rot q;
     double x = y;
     int n;
@@ -190,6 +226,13 @@ MRP_HD Rot rot(float y) {
         q.c = q.s;
     }
     return q;
+}
+
+// the entry point: the fast form below 120 rad, glibc's other branches (Payne-Hanek reduction,
+// inf/nan) out of the common path
+MRP_HD Rot rot(float y) {
+    if (abstop12(y) < abstop12(120.0f)) return rot_fast(y);
+    return rot_slow(y);
 }
 
 // ---------------------------------------------------------------------------------------

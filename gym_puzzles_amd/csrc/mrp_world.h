@@ -36,7 +36,11 @@ static __device__ unsigned long long g_stamps[16];     // per-phase sums over la
 static __device__ unsigned long long g_pmax[16];       // per-phase max over lane-steps
 static __device__ unsigned long long g_stepmax[256];   // per step (stepCounter mod 256): slowest lane's total
 static __device__ unsigned long long g_rt[2];          // sums of lane totals: s_memtime ticks, s_memrealtime ticks
-static __device__ uint32_t g_trace[16384][16];         // last step per lane: phases 0-10, total, nc, toi, pos, vel-units
+constexpr int MRP_TRACE_W = 24;
+static __device__ uint32_t g_trace[16384][MRP_TRACE_W];   // last step per lane: phases 0-10, total, nc, toi, pos, vel-units,
+                                                       // velocity / position / island-set-up cycles, largest island
+#define MRP_NOW() __builtin_amdgcn_s_memtime()
+#define MRP_SUB(k, t0) do { if (tid == 0) sh.trace[k] += (uint32_t)(__builtin_amdgcn_s_memtime() - (t0)); } while (0)
 #define MRP_TRACE(k, v) do { if (tid == 0) sh.trace[k] += (v); } while (0)
 #define MRP_STAMP(k)                                                                        \
     do {                                                                                    \
@@ -49,6 +53,8 @@ static __device__ uint32_t g_trace[16384][16];         // last step per lane: ph
 #else
 #define MRP_STAMP(k) MRP_PROG(0x100u * ((k) + 1))
 #define MRP_TRACE(k, v) do {} while (0)
+#define MRP_NOW() 0ull
+#define MRP_SUB(k, t0) do { (void)(t0); } while (0)
 #endif
 // Diagnostic hang localisation (build with -DMRP_PROGRESS; never in the shipped build): thread 0
 // of every lane stores the last progress point it reached into host-mapped memory, which a host
@@ -227,7 +233,7 @@ template <int ENV> struct Shared {
     double draws[D::NDRAW];
     unsigned long long stamp_t, stamp_t0, stamp_rt0;
 #ifdef MRP_STAMPS
-    uint32_t trace[16];
+    uint32_t trace[24];
 #endif
 };
 
@@ -694,7 +700,11 @@ template <int ENV> struct World {
             touching += __popcll(__ballot(t));
         }
         touching = __builtin_amdgcn_readfirstlane(touching);
+#ifdef MRP_PRIO_SIMPLE   // experiment switch: every lane with solver work at the top level
+        step_prio = touching >= 1 ? 3 : 0;
+#else
         step_prio = touching >= 4 ? 2 : (touching >= 2 ? 1 : 0);
+#endif
         if (prio_floor > step_prio) step_prio = prio_floor;
         set_prio(step_prio);
         __syncthreads();
@@ -770,7 +780,9 @@ template <int ENV> struct World {
             if (S.mtype[c] == MT_FACEA) {
                 normal = mul_rv(xA.q, v2(S.mlnx[c], S.mlny[c]));
                 V2 planePoint = mul_xv(xA, v2(S.mlpx[c], S.mlpy[c]));
-                for (int j = 0; j < mpcount; ++j) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {   // constant indices: pts stays in registers (no scratch)
+                    if (j >= mpcount) break;
                     V2 clipPoint = mul_xv(xB, v2(S.mpx[j][c], S.mpy[j][c]));
                     V2 pA = vadd(clipPoint, vmul(pc.rA - vdot(vsub(clipPoint, planePoint), normal), normal));
                     V2 pB = vsub(clipPoint, vmul(pc.rB, normal));
@@ -779,7 +791,9 @@ template <int ENV> struct World {
             } else {
                 normal = mul_rv(xB.q, v2(S.mlnx[c], S.mlny[c]));
                 V2 planePoint = mul_xv(xB, v2(S.mlpx[c], S.mlpy[c]));
-                for (int j = 0; j < mpcount; ++j) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if (j >= mpcount) break;
                     V2 clipPoint = mul_xv(xA, v2(S.mpx[j][c], S.mpy[j][c]));
                     V2 pB = vadd(clipPoint, vmul(pc.rB - vdot(vsub(clipPoint, planePoint), normal), normal));
                     V2 pA = vsub(clipPoint, vmul(pc.rA, normal));
@@ -788,7 +802,9 @@ template <int ENV> struct World {
                 normal = vneg(normal);
             }
             vc.nx = normal.x; vc.ny = normal.y;
-            for (int j = 0; j < vc.pointCount; ++j) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if (j >= vc.pointCount) break;
                 V2 rA = vsub(pts[j], cA), rB = vsub(pts[j], cB);
                 vc.rAx[j] = rA.x; vc.rAy[j] = rA.y; vc.rBx[j] = rB.x; vc.rBy[j] = rB.y;
                 float rnA = vcross(rA, normal), rnB = vcross(rB, normal);
@@ -989,13 +1005,14 @@ template <int ENV> struct World {
     __device__ __forceinline__ static int rdli(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
     // lane l of `old` replaced by the wave-uniform x (v_writelane_b32)
     __device__ __forceinline__ static float wrl(float old, float x, int l) { return __int_as_float(mrp_writelane(__float_as_int(x), l, __float_as_int(old))); }
-    __device__ __forceinline__ static bool fsame(float a, float b) { return __float_as_uint(a) == __float_as_uint(b); }
     // lane l's value of a per-lane condition, wave-uniform (ballot + bit test: no readlane)
     __device__ __forceinline__ static bool lane_bit(bool c, int l) { return (__builtin_amdgcn_ballot_w64(c) >> l) & 1ull; }
     // Early exit, exact: one sweep is a pure function of (body velocities, contact impulses), so
     // once the state after sweep k equals the state after sweep k-2 bit for bit the sequence has
     // period 1 or 2 from there on and the state after sweep `iters` is the state after sweep k
-    // whenever k and iters have the same parity.  The state is compared at exactly those k.
+    // whenever k and iters have the same parity.  The state is compared at the k with
+    // iters - k = 0 mod 4 against a snapshot taken two sweeps earlier (every fourth sweep rather
+    // than every second: the comparison is off the sweeps' dependency chain but not free).
     __device__ __forceinline__ int solver_velocity_lanes(Isl& is, VC* vcs, int iters, bool early_exit = true) {
         const int nc = is.nc;
         const VC& my = vcs[tid < nc ? tid : 0];   // lanes >= nc evaluate a copy of contact 0 and are never kept
@@ -1012,7 +1029,7 @@ template <int ENV> struct World {
         float bvx = is.vvx[bk], bvy = is.vvy[bk], bw = is.vw[bk];
         // state snapshot for the period check (taken at sweeps k with k = iters mod 2)
         float sni0 = ni0, sni1 = ni1, sti0 = ti0, sti1 = ti1, sbx = bvx, sby = bvy, sbw = bw;
-        bool have = (iters & 1) == 0;   // the initial state is sweep 0
+        bool have = snap_initial(iters);   // sweep 0 is a snapshot point
         const int ncu = __builtin_amdgcn_readfirstlane(nc);
         int sweeps = 0;
         for (int it = 0; it < iters; ++it) {
@@ -1109,12 +1126,15 @@ template <int ENV> struct World {
                 bvx = wrl(bvx, rdl(vA.x, i), ia); bvy = wrl(bvy, rdl(vA.y, i), ia); bw = wrl(bw, rdl(wA, i), ia);
                 bvx = wrl(bvx, rdl(vB.x, i), ib); bvy = wrl(bvy, rdl(vB.y, i), ib); bw = wrl(bw, rdl(wB, i), ib);
             }
-            if (early_exit && ((it + 1 - iters) & 1) == 0) {   // sweep it+1 has the parity of iters
-                if (have) {
-                    const bool same = fsame(ni0, sni0) && fsame(ni1, sni1) && fsame(ti0, sti0) && fsame(ti1, sti1) &&
-                                      fsame(bvx, sbx) && fsame(bvy, sby) && fsame(bw, sbw);
-                    if (__builtin_amdgcn_ballot_w64(!same) == 0) break;
-                }
+            const int left = iters - (it + 1);   // snapshot at left = 2 mod 4, compare at left = 0 mod 4 (see Snap)
+            if (early_exit && (left & 3) == 0 && have) {
+                const uint32_t d = (__float_as_uint(ni0) ^ __float_as_uint(sni0)) | (__float_as_uint(ni1) ^ __float_as_uint(sni1)) |
+                                   (__float_as_uint(ti0) ^ __float_as_uint(sti0)) | (__float_as_uint(ti1) ^ __float_as_uint(sti1)) |
+                                   (__float_as_uint(bvx) ^ __float_as_uint(sbx)) | (__float_as_uint(bvy) ^ __float_as_uint(sby)) |
+                                   (__float_as_uint(bw) ^ __float_as_uint(sbw));
+                if (__builtin_amdgcn_ballot_w64(d != 0u) == 0) break;
+            }
+            if (early_exit && (left & 3) == 2) {
                 sni0 = ni0; sni1 = ni1; sti0 = ti0; sti1 = ti1; sbx = bvx; sby = bvy; sbw = bw;
                 have = true;
             }
@@ -1234,32 +1254,46 @@ template <int ENV> struct World {
             }
         }
     }
-    // exact early exit (see solver_velocity_lanes): compare the state after sweep k with the
-    // snapshot from sweep k-2 at the sweeps of iters' parity; true = the remaining sweeps are no-ops
+    // exact early exit (see solver_velocity_lanes): the state after sweep k is compared with the
+    // snapshot of sweep k-2 at every sweep k with iters - k = 0 mod 4, the snapshot is taken at
+    // iters - k = 2 mod 4; true = the remaining sweeps are no-ops.  The comparison is one OR-tree
+    // of XORs of the bit patterns (wave-uniform values: any lane decides).
     template <int NS> struct Snap {
         float s[NS];
         bool have;
-        __device__ __forceinline__ bool check(const float (&cur)[NS]) {
-            bool same = have;
+        __device__ __forceinline__ void take(const float (&cur)[NS]) {
 #pragma unroll
-            for (int k = 0; k < NS; ++k) { same = same && fsame(cur[k], s[k]); s[k] = cur[k]; }
+            for (int k = 0; k < NS; ++k) s[k] = cur[k];
             have = true;
-            return uni(same);
+        }
+        __device__ __forceinline__ bool same(const float (&cur)[NS]) const {
+            uint32_t d = 0u;
+#pragma unroll
+            for (int k = 0; k < NS; ++k) d |= __float_as_uint(cur[k]) ^ __float_as_uint(s[k]);
+            return have && uni(d == 0u);
+        }
+        // one early-exit point after sweep `it + 1` of `iters`
+        __device__ __forceinline__ bool step(int it, int iters, const float (&cur)[NS]) {
+            const int left = iters - (it + 1);
+            if ((left & 3) == 0) return same(cur);
+            if ((left & 3) == 2) take(cur);
+            return false;
         }
     };
+    __device__ __forceinline__ static bool snap_initial(int iters) { return (iters & 3) == 2; }   // sweep 0 is a snapshot point
     __device__ __forceinline__ int solver_velocity_one(Isl& is, VC* vcs, int iters, bool early_exit = true) {
         CC c = load_cc(vcs[0]);
         const int ia = vcs[0].iaI, ib = vcs[0].ibI;
         V2 vA = v2(is.vvx[ia], is.vvy[ia]); float wA = is.vw[ia];
         V2 vB = v2(is.vvx[ib], is.vvy[ib]); float wB = is.vw[ib];
-        Snap<10> snap = {{vA.x, vA.y, wA, vB.x, vB.y, wB, c.ni0, c.ni1, c.ti0, c.ti1}, (iters & 1) == 0};
+        Snap<10> snap = {{vA.x, vA.y, wA, vB.x, vB.y, wB, c.ni0, c.ni1, c.ti0, c.ti1}, snap_initial(iters)};
         int sweeps = 0;
         for (int it = 0; it < iters; ++it) {
             ++sweeps;
             cc_update(c, vA, wA, vB, wB);
-            if (early_exit && ((it + 1 - iters) & 1) == 0) {
+            if (early_exit && ((iters - it - 1) & 1) == 0) {
                 const float cur[10] = {vA.x, vA.y, wA, vB.x, vB.y, wB, c.ni0, c.ni1, c.ti0, c.ti1};
-                if (snap.check(cur)) break;
+                if (snap.step(it, iters, cur)) break;
             }
         }
         if (tid == 0) {
@@ -1278,16 +1312,16 @@ template <int ENV> struct World {
         V2 vX = v2(is.vvx[x], is.vvy[x]), vY = v2(is.vvx[y], is.vvy[y]), vZ = v2(is.vvx[z], is.vvy[z]);
         float wX = is.vw[x], wY = is.vw[y], wZ = is.vw[z];
         Snap<17> snap = {{vX.x, vX.y, wX, vY.x, vY.y, wY, vZ.x, vZ.y, wZ, c0.ni0, c0.ni1, c0.ti0, c0.ti1,
-                          c1.ni0, c1.ni1, c1.ti0, c1.ti1}, (iters & 1) == 0};
+                          c1.ni0, c1.ni1, c1.ti0, c1.ti1}, snap_initial(iters)};
         int sweeps = 0;
         for (int it = 0; it < iters; ++it) {
             ++sweeps;
             if (XA0) cc_update(c0, vX, wX, vY, wY); else cc_update(c0, vY, wY, vX, wX);
             if (XA1) cc_update(c1, vX, wX, vZ, wZ); else cc_update(c1, vZ, wZ, vX, wX);
-            if (early_exit && ((it + 1 - iters) & 1) == 0) {
+            if (early_exit && ((iters - it - 1) & 1) == 0) {
                 const float cur[17] = {vX.x, vX.y, wX, vY.x, vY.y, wY, vZ.x, vZ.y, wZ, c0.ni0, c0.ni1, c0.ti0, c0.ti1,
                                        c1.ni0, c1.ni1, c1.ti0, c1.ti1};
-                if (snap.check(cur)) break;
+                if (snap.step(it, iters, cur)) break;
             }
         }
         if (tid == 0) {   // contact 1 stores last, as the reference's per-contact write-back order leaves it
@@ -1306,15 +1340,15 @@ template <int ENV> struct World {
         V2 vP = v2(is.vvx[p], is.vvy[p]), vQ = v2(is.vvx[q], is.vvy[q]);
         float wP = is.vw[p], wQ = is.vw[q];
         Snap<14> snap = {{vP.x, vP.y, wP, vQ.x, vQ.y, wQ, c0.ni0, c0.ni1, c0.ti0, c0.ti1, c1.ni0, c1.ni1, c1.ti0, c1.ti1},
-                         (iters & 1) == 0};
+                         snap_initial(iters)};
         int sweeps = 0;
         for (int it = 0; it < iters; ++it) {
             ++sweeps;
             cc_update(c0, vP, wP, vQ, wQ);
             if (SAME) cc_update(c1, vP, wP, vQ, wQ); else cc_update(c1, vQ, wQ, vP, wP);
-            if (early_exit && ((it + 1 - iters) & 1) == 0) {
+            if (early_exit && ((iters - it - 1) & 1) == 0) {
                 const float cur[14] = {vP.x, vP.y, wP, vQ.x, vQ.y, wQ, c0.ni0, c0.ni1, c0.ti0, c0.ti1, c1.ni0, c1.ni1, c1.ti0, c1.ti1};
-                if (snap.check(cur)) break;
+                if (snap.step(it, iters, cur)) break;
             }
         }
         if (tid == 0) {
@@ -1678,12 +1712,18 @@ template <int ENV> struct World {
                             stack[sc++] = other; bflag |= 1u << other;
                         }
                     }
+                    const unsigned long long tp = MRP_NOW();
                     island_pre(is, h, dtRatio, sh.u.sol.vcs, sh.u.sol.pcs);
+                    MRP_SUB(18, tp);
+#ifdef MRP_STAMPS
+                    if ((uint32_t)is.nc > sh.trace[19]) sh.trace[19] = (uint32_t)is.nc;
+#endif
                 }
             }
             __syncthreads();
             if (!sh.isl_go) break;
             const int nc = __builtin_amdgcn_readfirstlane(is.nc);
+            const unsigned long long tv = MRP_NOW();
             // the lanes with the most contact updates set the kernel's duration: let their
             // sweeps win the SIMD's issue arbitration over co-resident waves
             const int lvl = nc >= 6 ? 3 : (nc >= 4 ? 2 : (nc >= 2 ? 1 : 0));
@@ -1695,12 +1735,15 @@ template <int ENV> struct World {
                 (void)sweeps;
             }
             else if (nc > 64 && tid == 0) for (int it = 0; it < 180; ++it) solver_velocity(is, sh.u.sol.vcs);
+            MRP_SUB(16, tv);
             __syncthreads();
             MRP_PROG(0x3400u + nisl);
             if (tid == 0) island_mid(is, h, sh.u.sol.vcs);
             __syncthreads();
             MRP_PROG(0x3800u + nisl);
+            const unsigned long long tq = MRP_NOW();
             island_position(is, sh.u.sol.vcs, sh.u.sol.pcs, nc);
+            MRP_SUB(17, tq);
             if (nc > 0 && nc <= 64) set_prio(step_prio);
             __syncthreads();
             MRP_PROG(0x3c00u + nisl);

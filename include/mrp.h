@@ -155,8 +155,8 @@ int mrp_get_goals(mrp_ctx* ctx, double* out);
  * vertices x (x, y); unused entries 0 / fix_body -1) */
 int mrp_shapes(int env_id, int32_t* n_fix, int32_t* fix_body, int32_t* counts, float* verts);
 
-/* Device self-test of the glibc-faithful sinf/cosf used by every b2Rot::Set on the GPU:
- * evaluates them on device `device` for n host inputs (host output arrays). */
+/* Device self-test of the glibc-faithful sinf/cosf of every b2Rot::Set on the GPU: evaluates
+ * b2Rot::Set (sin, cos) as the step does on device `device` for n host inputs (host output arrays). */
 int mrp_selftest_sincos(int device, const float* x, float* sin_out, float* cos_out, int n);
 /* Diagnostic builds (-DMRP_STAMPS) only: per-phase cycle totals of thread 0 since the last call
  * (returns MRP_E_STATE in the shipped build). */
@@ -165,8 +165,9 @@ int mrp_debug_stamps(int device, uint64_t* out16);
  * (256 slots, indexed by step counter mod 256) and the (s_memtime, s_memrealtime) sums of lane
  * totals since the last call. */
 int mrp_debug_stamps_ext(int device, uint64_t* pmax16, uint64_t* stepmax256, uint64_t* rt2);
-/* Diagnostic builds only: the last step's per-lane trace, n_lanes x 16 words (phase cycles 0-10,
- * total, island contacts, TOI events, position iterations, velocity-solver contact units). */
+/* Diagnostic builds only: the last step's per-lane trace, n_lanes x 24 words (phase cycles 0-10,
+ * total, island contacts, TOI events, position iterations, velocity-solver contact units, then
+ * velocity-sweep / position-pass / island set-up cycles and the largest island's contacts). */
 int mrp_debug_trace(int device, uint32_t* out, int n_lanes);
 /* Diagnostic builds (-DMRP_PROGRESS) only: allocate n_lanes host-mapped words that every lane's
  * thread 0 overwrites with the last progress point it reached; readable while a launch runs

@@ -41,6 +41,7 @@ static double py_distance(double ax, double ay, double bx, double by) {
 
 float or_sinf(float x) { return sinf(x); }
 float or_cosf(float x) { return cosf(x); }
+void or_sincos_batch(const float* x, float* s, float* c, int n) { for (int i = 0; i < n; ++i) { s[i] = sinf(x[i]); c[i] = cosf(x[i]); } }
 
 /* ---------------------------------------------------------------- counter RNG (device-reset path) */
 static uint64_t splitmix64(uint64_t x) {

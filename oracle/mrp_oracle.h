@@ -51,6 +51,7 @@ long or_batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_t la
 /* glibc-faithful math exported for tests */
 float or_sinf(float x);
 float or_cosf(float x);
+void or_sincos_batch(const float* x, float* s, float* c, int n);   /* glibc sinf/cosf over an array */
 
 /* counter-based RNG shared with the device path (integer SplitMix64 mix) */
 double or_rng_u01(uint64_t seed, uint64_t lane, uint64_t stream, uint64_t counter);

@@ -66,6 +66,8 @@ def lib():
         L.or_sinf.restype = c_float
         L.or_cosf.argtypes = [c_float]
         L.or_cosf.restype = c_float
+        L.or_sincos_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.or_sincos_batch.restype = None
         L.or_rng_u01.argtypes = [ctypes.c_uint64] * 4
         L.or_rng_u01.restype = c_double
         L.or_body_mass.argtypes = [P, c_int, P]

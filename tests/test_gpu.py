@@ -213,21 +213,26 @@ def test_step_before_reset_fails_loudly(gpu_lib):
 
 
 def test_device_sincos_matches_glibc(gpu_lib, orc):
-    """The device sinf/cosf restatement equals the host glibc sinf/cosf (the oracle's)."""
+    """b2Rot::Set as the step evaluates it (mrp::rot: the branch-free form below 120 rad, glibc's
+    other branches above) equals the host glibc sinf/cosf (the oracle's) on every input: random
+    angles at several scales, random bit patterns (NaN, inf, subnormals included) and the range
+    thresholds (2^-12, pi/4, 120) and quadrant boundaries."""
     from gym_puzzles_amd._native import selftest_sincos
     rs = np.random.RandomState(0)
+    edges = np.array([2.0 ** -12, np.pi / 4, 120.0], np.float32)
+    near = (edges.view(np.int32)[:, None] + np.arange(-2000, 2001)[None, :]).astype(np.int32).view(np.float32).ravel()
     x = np.concatenate([
         rs.uniform(-10, 10, 200000), rs.uniform(-1e4, 1e4, 50000), rs.uniform(-1e30, 1e30, 2000),
         np.arange(-64, 65) * (np.pi / 4), np.array([0.0, -0.0, 1e-30, -1e-30, 1e-45, np.pi, 3e38, -3e38]),
     ]).astype(np.float32)
+    x = np.concatenate([x, near, -near, rs.randint(0, 2 ** 32, 300000, dtype=np.uint64).astype(np.uint32).view(np.float32)])
     s, c = selftest_sincos(x)
-    L = orc.lib()
-    step = 37
-    idx = np.r_[np.arange(0, x.size, step), np.arange(x.size - 200, x.size)]
-    es = np.array([L.or_sinf(float(x[i])) for i in idx], np.float32)
-    ec = np.array([L.or_cosf(float(x[i])) for i in idx], np.float32)
-    _eq("sinf", s[idx], es)
-    _eq("cosf", c[idx], ec)
+    es, ec = np.zeros_like(x), np.zeros_like(x)
+    orc.lib().or_sincos_batch(x.ctypes.data, es.ctypes.data, ec.ctypes.data, x.size)
+    for name, got, exp in (("sinf", s, es), ("cosf", c, ec)):
+        nan = np.isnan(exp)
+        assert np.array_equal(np.isnan(got), nan), name
+        _eq(name, got[~nan].view(np.uint32), exp[~nan].view(np.uint32))   # bit patterns: signed zeros count
 
 
 def test_step_device_with_torch_stream(gpu_lib):

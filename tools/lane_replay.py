@@ -15,13 +15,14 @@ NAMES = "load act fnc0 coll solve fnc1 toi obs out reset store".split()
 
 
 def trace(L, n):
-    tr = np.zeros((n, 16), np.uint32)
+    tr = np.zeros((n, 24), np.uint32)
     L.mrp_debug_trace(0, tr.ctypes.data_as(ctypes.c_void_p), n)
     return tr
 
 
 def row(r):
-    return f"{r[11]:9d} | " + " ".join(f"{v:7d}" for v in r[:11]) + f" | nc {r[12]} toi {r[13]} pos {r[14]} vel {r[15]}"
+    return (f"{r[11]:9d} | " + " ".join(f"{v:7d}" for v in r[:11]) + f" | nc {r[12]} toi {r[13]} pos {r[14]} vel {r[15]}"
+            f" | vel {r[16]} pos {r[17]} pre {r[18]} maxisl {r[19]}")
 
 
 env = int(sys.argv[1]) if len(sys.argv) > 1 else 0

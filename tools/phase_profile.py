@@ -42,7 +42,7 @@ def main():
           f"slowest lane per step: mean {sm.mean():.0f} max {sm.max():.0f} cyc ({sm.mean() / ghz / 1e3:.1f} us mean)")
     for i, n in enumerate(NAMES):
         print(f"  {n:20s} {buf[i] / lanes / steps:10.0f} cyc  {100 * buf[i] / tot:5.1f}%   max {pmax[i]:10d}")
-    tr = np.zeros((lanes, 16), np.uint32)
+    tr = np.zeros((lanes, 24), np.uint32)
     L.mrp_debug_trace(0, vp(tr), lanes)
     order = np.argsort(-tr[:, 11].astype(np.int64))
     print("  last step, slowest lanes: total | load act fnc0 coll solve fnc1 toi obs out reset store | nc toi pos velunits")
