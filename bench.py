@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--later-window", type=int, default=200,
                     help="diagnostic: also time this many steps starting near --later-start (0 = off; N=1 only)")
     ap.add_argument("--later-start", type=int, default=500)
+    ap.add_argument("--episode", type=int, default=1,
+                    help="diagnostic: also time one whole episode (TimeLimit steps from spawn, N=1 only; 0 = off)")
     ap.add_argument("--vecnormalize", action="store_true",
                     help="also run SB3 VecNormalize + Monitor statistics on the device every step (train.py:68,80-82)")
     args = ap.parse_args()
@@ -188,6 +190,21 @@ def main():
         first = args.warmup + K + skip + 1
         later = {"steps_after_spawn": [first, first + args.later_window - 1],
                  "env_steps_per_s": L * args.later_window / (s0.elapsed_time(s1) * 1e-3)}
+    # Diagnostic only (never `value`): one whole episode from spawn to the TimeLimit reset, every
+    # lane in lockstep as SB3's DummyVecEnv keeps them (v0 ends early only on puzzle completion):
+    # the rate averaged over every phase of an episode.
+    episode = None
+    if args.episode and rank == 0 and not distributed:
+        T = b.max_episode_steps
+        b.reset()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        e0.record(stream)
+        for _ in range(T):
+            one_step()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        episode = {"steps": T, "env_steps_per_s": L * T / (e0.elapsed_time(e1) * 1e-3)}
     if rank == 0:
         total_steps = world * L * K
         value = total_steps / elapsed
@@ -222,7 +239,7 @@ def main():
             "diagnostics": {"toi_events_total": toi, "position_iterations_total": pos,
                             "timed_steps_after_spawn": [args.warmup + 1, args.warmup + K],
                             "kernel_ms_min_median_max": [float(kts.min()), float(np.median(kts)), float(kts.max())],
-                            "later_window": later},
+                            "later_window": later, "whole_episode": episode},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.env, L, args.seed)

@@ -129,7 +129,10 @@ __global__ __launch_bounds__(BLOCK, 4) void k_reset(uint32_t* state, int nl, con
 }
 
 template <int ENV>
-__global__ __launch_bounds__(BLOCK, 4) void k_step(uint32_t* state, int nl, const float* actions, float* obs, float* reward,
+#ifndef MRP_STEP_WAVES_PER_EU
+#define MRP_STEP_WAVES_PER_EU 4   // 4 waves per SIMD: all 4096 lanes of a GPU resident at once (LDS allows 16 per CU)
+#endif
+__global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t* state, int nl, const float* actions, float* obs, float* reward,
                                                 double* reward64, uint8_t* done_out, uint8_t* trunc_out, uint8_t* status_out, float* term_obs,
                                                 EnvParams P, uint64_t seed, uint64_t lane_offset, int auto_reset,
                                                 int max_steps, const int* __restrict__ order, uint32_t* __restrict__ cost,

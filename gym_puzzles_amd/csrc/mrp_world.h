@@ -700,11 +700,7 @@ template <int ENV> struct World {
             touching += __popcll(__ballot(t));
         }
         touching = __builtin_amdgcn_readfirstlane(touching);
-#ifdef MRP_PRIO_SIMPLE   // experiment switch: every lane with solver work at the top level
-        step_prio = touching >= 1 ? 3 : 0;
-#else
         step_prio = touching >= 4 ? 2 : (touching >= 2 ? 1 : 0);
-#endif
         if (prio_floor > step_prio) step_prio = prio_floor;
         set_prio(step_prio);
         __syncthreads();

@@ -1,15 +1,17 @@
 #!/bin/bash
-# A/B of library builds on the GPU box: tools/ab_bench.sh libA.so libB.so ...  (bench 20/5 and 200/20, twice each, interleaved)
+# A/B of library builds (and schedule modes) on the GPU box, bench 20/5 and 200/20, twice each, interleaved:
+#   tools/ab_bench.sh libA.so[:mode] libB.so[:mode] ...
 set -uo pipefail
 mkdir -p gpurun_out
 out=gpurun_out/ab.txt; : > $out
-libs=("$@")
 for rep in 1 2; do
-  for lib in "${libs[@]}"; do
+  for spec in "$@"; do
+    lib=${spec%%:*}; mode=0
+    [[ "$spec" == *:* ]] && mode=${spec##*:}
     for cfg in "20 5" "200 20"; do
       read -r K W <<< "$cfg"
-      r=$(MRP_LIB=$lib timeout -k 5 120 python bench.py --steps $K --warmup $W --no-cpu-baseline --later-window 0 2>/dev/null | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('%.3fM' % (d['value']/1e6), 'kernel %.3f ms' % d['roofline']['kernel_ms'])") || { echo "bench failed for $lib"; exit 1; }
-      echo "$lib steps=$K warmup=$W: $r" | tee -a $out
+      r=$(MRP_LIB=$lib timeout -k 5 120 python bench.py --steps $K --warmup $W --no-cpu-baseline --later-window 0 --schedule $mode 2>/dev/null | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('%.3fM' % (d['value']/1e6), 'kernel %.3f ms' % d['roofline']['kernel_ms'])") || { echo "bench failed for $spec"; exit 1; }
+      echo "$spec steps=$K warmup=$W: $r" | tee -a $out
     done
   done
 done

@@ -4,7 +4,7 @@
 #   tools/collect_profiles.sh <round-tag>
 set -euo pipefail
 R=$1
-declare -A ENVS=([v0]="0 4096" [heavy_v0]="1 4096" [v2]="2 1024" [heavy_v2_3block]="4 1024")
+declare -A ENVS=([v0]="0 4096" [heavy_v0]="1 4096" [v2]="2 1024" [heavy_v2_3block]="4 1024" [v3]="5 4096")
 for k in "${!ENVS[@]}"; do
   set -- ${ENVS[$k]}
   D=gpurun_out/prof_${R}_$k
@@ -14,3 +14,4 @@ for k in "${!ENVS[@]}"; do
   grep -h '"metric"' $D/kt.log > profiles/${R}_${k}_bench_under_rocprof.json
 done
 grep -h '"metric"' gpurun_out/bench_default.log > profiles/${R}_bench_default.json
+grep -h '"metric"' gpurun_out/bench_driver.log > profiles/${R}_bench_driver_window.json

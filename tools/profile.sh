@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT profiles
 LANES=${LANES:-4096}
-ARGS="--steps 100 --warmup 10 --no-cpu-baseline --later-window 0 --env $ENV --lanes $LANES $*"
+ARGS="--steps 100 --warmup 10 --no-cpu-baseline --later-window 0 --episode 0 --env $ENV --lanes $LANES $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 bench.py $ARGS > $OUT/kt.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- python3 bench.py $ARGS > $OUT/write.log 2>&1
