@@ -1712,7 +1712,14 @@ template <int ENV> struct World {
                     island_pre(is, h, dtRatio, sh.u.sol.vcs, sh.u.sol.pcs);
                     MRP_SUB(18, tp);
 #ifdef MRP_STAMPS
-                    if ((uint32_t)is.nc > sh.trace[19]) sh.trace[19] = (uint32_t)is.nc;
+                    if ((uint32_t)is.nc > sh.trace[19]) {   // largest island: its contacts' bodies (A << 8 | B)
+                        sh.trace[19] = (uint32_t)is.nc;
+                        for (int k = 0; k < 4; ++k) {
+                            const int c = k < is.nc ? is.contacts[k] : -1;
+                            sh.trace[20 + k] = c < 0 ? 0xffffffffu
+                                             : ((uint32_t)L.fix_body[S.cfa[c]] << 8) | (uint32_t)L.fix_body[S.cfb[c]];
+                        }
+                    }
 #endif
                 }
             }

@@ -22,7 +22,8 @@ def trace(L, n):
 
 def row(r):
     return (f"{r[11]:9d} | " + " ".join(f"{v:7d}" for v in r[:11]) + f" | nc {r[12]} toi {r[13]} pos {r[14]} vel {r[15]}"
-            f" | vel {r[16]} pos {r[17]} pre {r[18]} maxisl {r[19]}")
+            f" | vel {r[16]} pos {r[17]} pre {r[18]} maxisl {r[19]} "
+            + " ".join(f"{(v >> 8) & 255}-{v & 255}" for v in r[20:24] if v != 0xffffffff))
 
 
 env = int(sys.argv[1]) if len(sys.argv) > 1 else 0
