@@ -46,19 +46,21 @@ class StepGather:
         L = shard.lanes_per_rank
         self.packed = torch.zeros((L, obs_dim + 2), dtype=torch.float32, device=device)
         root = shard.rank == 0 or to_all
-        self.blocks = [torch.zeros_like(self.packed) for _ in range(shard.world)] if root else None
+        # the receive blocks are row slices of ONE [G, obs_dim + 2] buffer: the gathered step is
+        # contiguous on arrival, no concatenation afterwards
+        self.full = torch.zeros((shard.global_lanes, obs_dim + 2), dtype=torch.float32, device=device) if root else None
+        self.blocks = list(self.full.split(L, dim=0)) if root else None
 
     def pack(self, obs, reward, done):
-        O = self.obs_dim
-        self.packed[:, :O].copy_(obs)
-        self.packed[:, O].copy_(reward)
-        self.packed[:, O + 1].copy_(done)
+        import torch
+        # one fused copy into the packed rows [obs | reward | done]
+        torch.cat((obs, reward.unsqueeze(1), done.unsqueeze(1).to(torch.float32)), dim=1, out=self.packed)
         return self.packed
 
     def __call__(self, obs, reward, done):
         """Returns (obs [G, O], reward [G], done [G]) over all G global lanes on rank 0 (every
-        rank with to_all), None elsewhere.  Single-process: no collective."""
-        import torch
+        rank with to_all), None elsewhere.  Single-process: no collective.  The returned tensors
+        are views of this gatherer's receive buffer, valid until its next call."""
         import torch.distributed as dist
         p = self.pack(obs, reward, done)
         if self.shard.world == 1:
@@ -70,6 +72,6 @@ class StepGather:
                 dist.gather(p, self.blocks if self.shard.rank == 0 else None, dst=0, group=self.group)
             if self.blocks is None:
                 return None
-            full = torch.cat(self.blocks, dim=0)
+            full = self.full
         O = self.obs_dim
         return full[:, :O], full[:, O], full[:, O + 1] != 0
