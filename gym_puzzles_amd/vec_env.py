@@ -224,10 +224,14 @@ class MultiRobotPuzzleVecNormalize:
     (normalised), ``TimeLimit.truncated`` and Monitor's ``episode`` = {"r", "l"} for finished
     lanes; ``get_original_obs()`` / ``get_original_reward()`` give the raw values."""
 
-    def __init__(self, venv: MultiRobotPuzzleVecEnv, training: bool = True, clip_obs: float = 10.0,
-                 clip_reward: float = 10.0, gamma: float = 0.99, epsilon: float = 1e-8):
+    def __init__(self, venv: MultiRobotPuzzleVecEnv, training: bool = True, norm_obs: bool = True, norm_reward: bool = True,
+                 clip_obs: float = 10.0, clip_reward: float = 10.0, gamma: float = 0.99, epsilon: float = 1e-8):
         import torch
         self.venv = venv
+        # SB3 semantics: the flags choose what step()/reset() return; the running statistics are
+        # updated whenever `training` is set, whatever the flags
+        self.norm_obs, self.norm_reward = bool(norm_obs), bool(norm_reward)
+        self.clip_obs, self.clip_reward, self.gamma, self.epsilon = clip_obs, clip_reward, gamma, epsilon
         self.num_envs, self.observation_space, self.action_space = venv.num_envs, venv.observation_space, venv.action_space
         N, O = venv.num_envs, venv.observation_space.shape[0]
         dev = torch.device("cuda", venv.device)
@@ -252,7 +256,7 @@ class MultiRobotPuzzleVecNormalize:
         import torch
         self._obs.copy_(torch.from_numpy(self.venv.reset()))
         self.norm.reset(self._obs, self._nobs)
-        return self._nobs.cpu().numpy()
+        return (self._nobs if self.norm_obs else self._obs).cpu().numpy()
 
     def step(self, actions):
         import torch
@@ -260,12 +264,14 @@ class MultiRobotPuzzleVecNormalize:
         self.venv.step_torch(self._act, self._obs, self._rew, self._done, self._trunc, self._term, self._rew64)
         self.norm.step(self._obs, self._rew, self._done, self._nobs, self._nrew, self._term, self._nterm, self._epr, self._epl,
                        self._rew64)
-        obs, rew = self._nobs.cpu().numpy(), self._nrew.cpu().numpy()
+        obs = (self._nobs if self.norm_obs else self._obs).cpu().numpy()
+        rew = (self._nrew if self.norm_reward else self._rew).cpu().numpy()
         done, trunc = self._done.cpu().numpy().astype(bool), self._trunc.cpu().numpy().astype(bool)
         infos = [{} for _ in range(self.num_envs)]
         idx = np.nonzero(done)[0]
         if idx.size:
-            term, epr, epl = self._nterm.cpu().numpy(), self._epr.cpu().numpy(), self._epl.cpu().numpy()
+            term = (self._nterm if self.norm_obs else self._term).cpu().numpy()
+            epr, epl = self._epr.cpu().numpy(), self._epl.cpu().numpy()
             for i in idx:
                 infos[i]["terminal_observation"] = term[i].copy()
                 infos[i]["TimeLimit.truncated"] = bool(trunc[i])
@@ -275,8 +281,38 @@ class MultiRobotPuzzleVecNormalize:
     def get_original_obs(self):
         return self._obs.cpu().numpy()
 
+    # ---- persistence (SB3's VecNormalize.save / VecNormalize.load, train/test.py:66) --------
+    # SB3 pickles the wrapper; this build stores the same statistics and settings in an .npz
+    # (nothing in the file is executed on load).
+    def save(self, save_path: str) -> None:
+        st = self.norm.get_stats()
+        np.savez(save_path, **st, clip_obs=self.clip_obs, clip_reward=self.clip_reward, gamma=self.gamma,
+                 epsilon=self.epsilon, training=self.training, norm_obs=self.norm_obs, norm_reward=self.norm_reward)
+
+    @classmethod
+    def load(cls, load_path: str, venv: MultiRobotPuzzleVecEnv) -> "MultiRobotPuzzleVecNormalize":
+        with np.load(load_path, allow_pickle=False) as z:
+            d = {k: z[k] for k in z.files}
+        self = cls(venv, training=bool(d["training"]), norm_obs=bool(d["norm_obs"]), norm_reward=bool(d["norm_reward"]),
+                   clip_obs=float(d["clip_obs"]), clip_reward=float(d["clip_reward"]), gamma=float(d["gamma"]),
+                   epsilon=float(d["epsilon"]))
+        self.norm.set_stats({k: d[k] for k in ("obs_mean", "obs_var", "obs_count", "ret_mean", "ret_var", "ret_count")})
+        return self
+
+    def get_stats(self) -> dict:
+        return self.norm.get_stats()
+
     def get_original_reward(self):
         return self._rew.cpu().numpy()
+
+    def get_images(self):   # VecEnvWrapper passes rendering through (VecVideoRecorder, test.py:61-63)
+        return self.venv.get_images()
+
+    def env_method(self, method_name, *args, indices=None, **kwargs):
+        return self.venv.env_method(method_name, *args, indices=indices, **kwargs)
+
+    def get_attr(self, attr_name, indices=None):
+        return self.venv.get_attr(attr_name, indices)
 
     def close(self):
         self.norm.close()

@@ -156,3 +156,40 @@ def test_monitor_sums_the_float64_rewards(gpu_lib):
     assert n_done >= 2 * lanes
     norm.close()
     b.close()
+
+
+@pytest.mark.gpu
+def test_vecnormalize_save_load_and_eval_flags(gpu_lib, tmp_path):
+    """train/test.py:66-68's flow: VecNormalize.load(path, env); env.training = False;
+    env.norm_reward = False.  The loaded wrapper carries the saved statistics bit for bit, stops
+    updating them once training is off, and returns raw rewards with norm_reward off (raw obs with
+    norm_obs off) while the normalised values stay what the statistics give."""
+    from gym_puzzles_amd import MultiRobotPuzzleVecEnv, MultiRobotPuzzleVecNormalize
+    rs = np.random.RandomState(3)
+    act = lambda: rs.uniform(-1, 1, size=(64, 6)).astype(np.float32)  # noqa: E731
+    env = MultiRobotPuzzleVecNormalize(MultiRobotPuzzleVecEnv("MultiRobotPuzzle-v0", 64, seed=5, max_episode_steps=20))
+    env.reset()
+    for _ in range(30):
+        env.step(act())
+    path = str(tmp_path / "saved_env.npz")
+    env.save(path)
+    st = env.get_stats()
+    env.close()
+
+    ev = MultiRobotPuzzleVecNormalize.load(path, MultiRobotPuzzleVecEnv("MultiRobotPuzzle-v0", 64, seed=9,
+                                                                        max_episode_steps=20))
+    for k, v in st.items():
+        np.testing.assert_array_equal(ev.get_stats()[k], v)
+    ev.training = False
+    ev.norm_reward = False
+    ev.reset()
+    for _ in range(25):
+        o, r, d, infos = ev.step(act())
+        np.testing.assert_array_equal(r, ev.get_original_reward())   # raw rewards
+        assert np.all(np.abs(o) <= ev.clip_obs)
+    for k, v in st.items():   # training off: the statistics did not move
+        np.testing.assert_array_equal(ev.get_stats()[k], v)
+    ev.norm_obs = False
+    o, r, d, infos = ev.step(act())
+    np.testing.assert_array_equal(o, ev.get_original_obs())
+    ev.close()
