@@ -283,3 +283,33 @@ def test_costliest_first_schedule_changes_nothing(gpu_lib):
     _eq("state", a.get_state(), b.get_state())
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("env_id", ENVS)
+def test_whole_episode_soak(gpu_lib, orc, env_id):
+    """One whole episode at the registered TimeLimit (2000 / 3000 / 1500 steps) plus 50 steps of
+    the next, on the device-RNG + auto-reset path the bench runs: every lane reaches its TimeLimit
+    reset (or an earlier done), no loop guard trips, every observation stays finite, and the final
+    body state and per-lane reward sums equal the oracle's batch runner bit for bit."""
+    from gym_puzzles_amd import Batch
+    lanes = 4096 if env_id in (0, 5) else 1024
+    b = Batch(env_id, lanes, seed=23)
+    steps = b.max_episode_steps + 50
+    b.set_auto_reset(True)
+    b.reset()
+    rsum = np.zeros(lanes, np.float64)
+    ended = np.zeros(lanes, bool)
+    for _ in range(steps):
+        obs, rew, done, _ = b.step()
+        assert np.isfinite(obs).all()
+        rsum += rew.astype(np.float64)
+        ended |= done.astype(bool)
+    assert ended.all()
+    assert not b.faults().any(), "a loop guard tripped"
+    threads = min(16, os.cpu_count() or 1)
+    n, _, bodies, orsum, _ = orc.batch_run(env_id, lanes, steps, 23, draw_bounds(env_id), threads=threads,
+                                           outputs=True, max_steps=b.max_episode_steps)
+    assert n == lanes * steps
+    _eq("bodies", b.bodies(), bodies)
+    _eq("reward sums", rsum, orsum)
+    b.close()
