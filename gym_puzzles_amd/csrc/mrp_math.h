@@ -51,6 +51,28 @@ MRP_HD V2 mulT_xv(Xf T, V2 v) {
 MRP_HD Rot mulT_rr(Rot q, Rot r) { Rot o; o.s = q.c * r.s - q.s * r.c; o.c = q.c * r.c + q.s * r.s; return o; }
 MRP_HD Xf mulT_xx(Xf A, Xf B) { Xf C; C.q = mulT_rr(A.q, B.q); C.p = mulT_rv(A.q, vsub(B.p, A.p)); return C; }
 
+// Packed pairs for the solver loops: a native 2 x f32 vector, so the x and y halves of one
+// b2Vec2 operation issue as ONE v_pk_add_f32 / v_pk_mul_f32 (two IEEE f32 operations, each
+// rounded exactly like the scalar one; -ffp-contract=off keeps v_pk_fma_f32 out).  Broadcasts,
+// half swaps and negations fold into the instruction's op_sel / neg modifiers.  Every helper
+// computes each component with the operations, operands and order of its V2 counterpart above:
+//   pcross_sv(s, r) = s * (-r.y, r.x) = (-(s*r.y), s*r.x) = vcross_sv(s, r)  (negation is exact)
+//   pcross(a, b)    = (a * b.yx).x - (a * b.yx).y = a.x*b.y - a.y*b.x      = vcross(a, b)
+//   pcrossp(pperp(a), b) = a.x*b.y + -(a.y*b.x)                           = vcross(a, b)
+//   pdot(a, b)      = (a * b).x + (a * b).y                               = vdot(a, b)
+//   pmul_rv(q, v)   = (c,s)*v.x + (-s,c)*v.y = (c*vx - s*vy, s*vx + c*vy)  = mul_rv(q, v)
+typedef float P2 __attribute__((ext_vector_type(2)));
+MRP_HD P2 p2(float x, float y) { P2 r = {x, y}; return r; }
+MRP_HD P2 pbc(float s) { P2 r = {s, s}; return r; }
+MRP_HD P2 pperp(P2 r) { P2 o = {-r.y, r.x}; return o; }
+MRP_HD P2 pcross_sv(float s, P2 r) { return pbc(s) * pperp(r); }
+MRP_HD float pcross(P2 a, P2 b) { const P2 p = a * b.yx; return p.x - p.y; }
+// cross(a, b) from ap = pperp(a): ap * b = (-(a.y*b.x), a.x*b.y), and a.x*b.y + -(a.y*b.x) is
+// a.x*b.y - a.y*b.x exactly; with the arms stored as perps, pcross_sv(s, a) is one pbc(s) * ap
+MRP_HD float pcrossp(P2 ap, P2 b) { const P2 p = ap * b; return p.y + p.x; }
+MRP_HD float pdot(P2 a, P2 b) { const P2 p = a * b; return p.x + p.y; }
+MRP_HD P2 pmul_rv(Rot q, P2 v) { const P2 cs = {q.c, q.s}, sc = {-q.s, q.c}; return cs * pbc(v.x) + sc * pbc(v.y); }
+
 // ---------------------------------------------------------------------------------------
 // sinf / cosf, bit-exact with glibc >= 2.28's FMA code path (sysdeps/ieee754/flt-32
 // s_sinf.c / s_cosf.c, the variant glibc's ifunc selects on every FMA-capable x86-64 CPU).

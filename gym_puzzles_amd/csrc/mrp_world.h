@@ -1011,20 +1011,13 @@ template <int ENV> struct World {
     // than every second: the comparison is off the sweeps' dependency chain but not free).
     __device__ __forceinline__ int solver_velocity_lanes(Isl& is, VC* vcs, int iters, bool early_exit = true) {
         const int nc = is.nc;
-        const VC& my = vcs[tid < nc ? tid : 0];   // lanes >= nc evaluate a copy of contact 0 and are never kept
-        const float rAx0 = my.rAx[0], rAy0 = my.rAy[0], rBx0 = my.rBx[0], rBy0 = my.rBy[0];
-        const float rAx1 = my.rAx[1], rAy1 = my.rAy[1], rBx1 = my.rBx[1], rBy1 = my.rBy[1];
-        const float nmass0 = my.nmass[0], nmass1 = my.nmass[1], tmass0 = my.tmass[0], tmass1 = my.tmass[1];
-        const float vbias0 = my.vbias[0], vbias1 = my.vbias[1];
-        const float cnx = my.nx, cny = my.ny, k0 = my.k0, k1 = my.k1, k2 = my.k1, k3 = my.k3;
-        const float nm0 = my.nm0, nm1 = my.nm1, nm2 = my.nm1, nm3 = my.nm3;
-        const float cmA = my.mA, cmB = my.mB, ciA = my.iA, ciB = my.iB, cfr = my.friction;
-        const int cia = my.iaI, cib = my.ibI, cpc = my.pointCount;
-        float ni0 = my.ni[0], ni1 = my.ni[1], ti0 = my.ti[0], ti1 = my.ti[1];
+        CC my = load_cc(vcs[tid < nc ? tid : 0]);   // lanes >= nc evaluate a copy of contact 0 and are never kept
+        const int cia = vcs[tid < nc ? tid : 0].iaI, cib = vcs[tid < nc ? tid : 0].ibI;
         const int bk = tid < is.nb ? tid : 0;
         float bvx = is.vvx[bk], bvy = is.vvy[bk], bw = is.vw[bk];
         // state snapshot for the period check (taken at sweeps k with k = iters mod 2)
-        float sni0 = ni0, sni1 = ni1, sti0 = ti0, sti1 = ti1, sbx = bvx, sby = bvy, sbw = bw;
+        P2 sni = my.ni, sti = my.ti;
+        float sbx = bvx, sby = bvy, sbw = bw;
         bool have = snap_initial(iters);   // sweep 0 is a snapshot point
         const int ncu = __builtin_amdgcn_readfirstlane(nc);
         int sweeps = 0;
@@ -1033,110 +1026,33 @@ template <int ENV> struct World {
             for (int i = 0; i < ncu; ++i) {
                 // every lane evaluates ITS contact's update from contact i's body velocities;
                 // only lane i's result is kept (the Gauss-Seidel order is contact by contact)
-                const int ia = rdli(cia, i), ib = rdli(cib, i), pcount = rdli(cpc, i);
-                const bool mine = tid == i;
-                V2 vA = v2(rdl(bvx, ia), rdl(bvy, ia)); float wA = rdl(bw, ia);
-                V2 vB = v2(rdl(bvx, ib), rdl(bvy, ib)); float wB = rdl(bw, ib);
-                const float mA = cmA, iA = ciA, mB = cmB, iB = ciB;
-                V2 normal = v2(cnx, cny), tangent = vcross_vs(normal, 1.0f);
-                const float friction = cfr;
-                {   // friction, point 0
-                    V2 rA = v2(rAx0, rAy0), rB = v2(rBx0, rBy0);
-                    V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
-                    float vt = vdot(dv, tangent);
-                    float lambda = tmass0 * (-vt);
-                    float maxFriction = friction * ni0;
-                    float newImpulse = fclamp(ti0 + lambda, -maxFriction, maxFriction);
-                    lambda = newImpulse - ti0;
-                    if (mine) ti0 = newImpulse;
-                    V2 P = vmul(lambda, tangent);
-                    vA = vsub(vA, vmul(mA, P));
-                    wA -= iA * vcross(rA, P);
-                    vB = vadd(vB, vmul(mB, P));
-                    wB += iB * vcross(rB, P);
-                }
-                if (pcount == 2) {   // friction, point 1
-                    V2 rA = v2(rAx1, rAy1), rB = v2(rBx1, rBy1);
-                    V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
-                    float vt = vdot(dv, tangent);
-                    float lambda = tmass1 * (-vt);
-                    float maxFriction = friction * ni1;
-                    float newImpulse = fclamp(ti1 + lambda, -maxFriction, maxFriction);
-                    lambda = newImpulse - ti1;
-                    if (mine) ti1 = newImpulse;
-                    V2 P = vmul(lambda, tangent);
-                    vA = vsub(vA, vmul(mA, P));
-                    wA -= iA * vcross(rA, P);
-                    vB = vadd(vB, vmul(mB, P));
-                    wB += iB * vcross(rB, P);
-                }
-                if (pcount == 1) {
-                    V2 rA = v2(rAx0, rAy0), rB = v2(rBx0, rBy0);
-                    V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
-                    float vn = vdot(dv, normal);
-                    float lambda = -nmass0 * (vn - vbias0);
-                    float newImpulse = fmax_(ni0 + lambda, 0.0f);
-                    lambda = newImpulse - ni0;
-                    if (mine) ni0 = newImpulse;
-                    V2 P = vmul(lambda, normal);
-                    vA = vsub(vA, vmul(mA, P));
-                    wA -= iA * vcross(rA, P);
-                    vB = vadd(vB, vmul(mB, P));
-                    wB += iB * vcross(rB, P);
-                } else {
-                    V2 r1A = v2(rAx0, rAy0), r1B = v2(rBx0, rBy0);
-                    V2 r2A = v2(rAx1, rAy1), r2B = v2(rBx1, rBy1);
-                    V2 a = v2(ni0, ni1);
-                    V2 dv1 = vsub(vsub(vadd(vB, vcross_sv(wB, r1B)), vA), vcross_sv(wA, r1A));
-                    V2 dv2 = vsub(vsub(vadd(vB, vcross_sv(wB, r2B)), vA), vcross_sv(wA, r2A));
-                    float vn1 = vdot(dv1, normal), vn2 = vdot(dv2, normal);
-                    V2 b = v2(vn1 - vbias0, vn2 - vbias1);
-                    b = vsub(b, v2(k0 * a.x + k2 * a.y, k1 * a.x + k3 * a.y));
-                    // the block solver's case is decided by lane i's values (wave-uniform
-                    // branches); the other lanes follow lane i's case and are discarded
-                    V2 x = vneg(v2(nm0 * b.x + nm2 * b.y, nm1 * b.x + nm3 * b.y));
-                    bool ok = true;
-                    if (!lane_bit(x.x >= 0.0f && x.y >= 0.0f, i)) {
-                        x.x = -nmass0 * b.x; x.y = 0.0f;
-                        vn2 = k1 * x.x + b.y;
-                        if (!lane_bit(x.x >= 0.0f && vn2 >= 0.0f, i)) {
-                            x.x = 0.0f; x.y = -nmass1 * b.y;
-                            vn1 = k2 * x.y + b.x;
-                            if (!lane_bit(x.y >= 0.0f && vn1 >= 0.0f, i)) {
-                                x.x = 0.0f; x.y = 0.0f;
-                                ok = lane_bit(b.x >= 0.0f && b.y >= 0.0f, i);
-                            }
-                        }
-                    }
-                    if (ok) {
-                        V2 d = vsub(x, a);
-                        V2 P1 = vmul(d.x, normal), P2 = vmul(d.y, normal);
-                        vA = vsub(vA, vmul(mA, vadd(P1, P2)));
-                        wA -= iA * (vcross(r1A, P1) + vcross(r2A, P2));
-                        vB = vadd(vB, vmul(mB, vadd(P1, P2)));
-                        wB += iB * (vcross(r1B, P1) + vcross(r2B, P2));
-                        if (mine) { ni0 = x.x; ni1 = x.y; }
-                    }
-                }
+                const int ia = rdli(cia, i), ib = rdli(cib, i), pcount = rdli(my.pcount, i);
+                P2 vA = p2(rdl(bvx, ia), rdl(bvy, ia)); float wA = rdl(bw, ia);
+                P2 vB = p2(rdl(bvx, ib), rdl(bvy, ib)); float wB = rdl(bw, ib);
+                P2 ni, ti;
+                // the block solver's case is decided by lane i's values (wave-uniform branches);
+                // the other lanes follow lane i's case and are discarded
+                vel_update(my, pcount, [i](bool x) { return lane_bit(x, i); }, ni, ti, vA, wA, vB, wB);
+                if (tid == i) { my.ni = ni; my.ti = ti; }
                 // lane i's results go to the lanes of bodies A and B (A first, as the reference stores)
                 bvx = wrl(bvx, rdl(vA.x, i), ia); bvy = wrl(bvy, rdl(vA.y, i), ia); bw = wrl(bw, rdl(wA, i), ia);
                 bvx = wrl(bvx, rdl(vB.x, i), ib); bvy = wrl(bvy, rdl(vB.y, i), ib); bw = wrl(bw, rdl(wB, i), ib);
             }
             const int left = iters - (it + 1);   // snapshot at left = 2 mod 4, compare at left = 0 mod 4 (see Snap)
             if (early_exit && (left & 3) == 0 && have) {
-                const uint32_t d = (__float_as_uint(ni0) ^ __float_as_uint(sni0)) | (__float_as_uint(ni1) ^ __float_as_uint(sni1)) |
-                                   (__float_as_uint(ti0) ^ __float_as_uint(sti0)) | (__float_as_uint(ti1) ^ __float_as_uint(sti1)) |
+                const uint32_t d = (__float_as_uint(my.ni.x) ^ __float_as_uint(sni.x)) | (__float_as_uint(my.ni.y) ^ __float_as_uint(sni.y)) |
+                                   (__float_as_uint(my.ti.x) ^ __float_as_uint(sti.x)) | (__float_as_uint(my.ti.y) ^ __float_as_uint(sti.y)) |
                                    (__float_as_uint(bvx) ^ __float_as_uint(sbx)) | (__float_as_uint(bvy) ^ __float_as_uint(sby)) |
                                    (__float_as_uint(bw) ^ __float_as_uint(sbw));
                 if (__builtin_amdgcn_ballot_w64(d != 0u) == 0) break;
             }
             if (early_exit && (left & 3) == 2) {
-                sni0 = ni0; sni1 = ni1; sti0 = ti0; sti1 = ti1; sbx = bvx; sby = bvy; sbw = bw;
+                sni = my.ni; sti = my.ti; sbx = bvx; sby = bvy; sbw = bw;
                 have = true;
             }
         }
         if (tid < is.nb) { is.vvx[tid] = bvx; is.vvy[tid] = bvy; is.vw[tid] = bw; }
-        if (tid < nc) { VC& o = vcs[tid]; o.ni[0] = ni0; o.ni[1] = ni1; o.ti[0] = ti0; o.ti[1] = ti1; }
+        if (tid < nc) store_cc(vcs[tid], my);
         return sweeps;
     }
 
@@ -1147,126 +1063,147 @@ template <int ENV> struct World {
     // wave-uniform branches (ballot of identical lanes).  Same float operations in the same order
     // as solver_velocity, same exact early exit as solver_velocity_lanes.
     __device__ __forceinline__ static bool uni(bool c) { return __builtin_amdgcn_ballot_w64(c) != 0; }
-    struct CC {   // one contact's velocity-constraint constants (VC), in registers
-        float rAx0, rAy0, rBx0, rBy0, rAx1, rAy1, rBx1, rBy1, nmass0, nmass1, tmass0, tmass1, vbias0, vbias1;
-        float k0, k1, k3, nm0, nm1, nm3, mA, iA, mB, iB, friction;
-        V2 normal, tangent;
+    // One contact's velocity-constraint constants (VC) in registers, as packed pairs (P2: one
+    // v_pk_* instruction for both halves of a b2Vec2 operation) and the impulses (the state).
+    struct CC {
+        P2 rA0, rB0, rA1, rB1;   // arms of points 0 and 1, stored as pperp(r) = (-r.y, r.x) (see pcrossp)
+        P2 normal, tangent, vbias, k01, k13, nm01, nm13;   // K = [k0 k1; k1 k3], K^-1 = [nm0 nm1; nm1 nm3]
+        P2 mA, mB;   // (mA, mA), (mB, mB): broadcast once, not re-splatted (and hoisted into extra pairs) per use
+        float nmass0, nmass1, tmass0, tmass1, iA, iB, friction;
         int pcount;
-        float ni0, ni1, ti0, ti1;   // impulses (state)
+        P2 ni, ti;   // normal / tangent impulses of points 0 and 1
     };
     __device__ __forceinline__ static CC load_cc(const VC& c) {
         CC o;
-        o.rAx0 = c.rAx[0]; o.rAy0 = c.rAy[0]; o.rBx0 = c.rBx[0]; o.rBy0 = c.rBy[0];
-        o.rAx1 = c.rAx[1]; o.rAy1 = c.rAy[1]; o.rBx1 = c.rBx[1]; o.rBy1 = c.rBy[1];
+        o.rA0 = p2(-c.rAy[0], c.rAx[0]); o.rB0 = p2(-c.rBy[0], c.rBx[0]);
+        o.rA1 = p2(-c.rAy[1], c.rAx[1]); o.rB1 = p2(-c.rBy[1], c.rBx[1]);
+        o.normal = p2(c.nx, c.ny);
+        const V2 t = vcross_vs(v2(c.nx, c.ny), 1.0f);
+        o.tangent = p2(t.x, t.y);
+        o.vbias = p2(c.vbias[0], c.vbias[1]);
+        o.k01 = p2(c.k0, c.k1); o.k13 = p2(c.k1, c.k3); o.nm01 = p2(c.nm0, c.nm1); o.nm13 = p2(c.nm1, c.nm3);
         o.nmass0 = c.nmass[0]; o.nmass1 = c.nmass[1]; o.tmass0 = c.tmass[0]; o.tmass1 = c.tmass[1];
-        o.vbias0 = c.vbias[0]; o.vbias1 = c.vbias[1];
-        o.k0 = c.k0; o.k1 = c.k1; o.k3 = c.k3; o.nm0 = c.nm0; o.nm1 = c.nm1; o.nm3 = c.nm3;
-        o.mA = c.mA; o.iA = c.iA; o.mB = c.mB; o.iB = c.iB; o.friction = c.friction;
-        o.normal = v2(c.nx, c.ny); o.tangent = vcross_vs(o.normal, 1.0f);
-        o.pcount = __builtin_amdgcn_readfirstlane(c.pointCount);
-        o.ni0 = c.ni[0]; o.ni1 = c.ni[1]; o.ti0 = c.ti[0]; o.ti1 = c.ti[1];
+        o.mA = pbc(c.mA); o.iA = c.iA; o.mB = pbc(c.mB); o.iB = c.iB; o.friction = c.friction;
+        o.pcount = c.pointCount;
+        o.ni = p2(c.ni[0], c.ni[1]); o.ti = p2(c.ti[0], c.ti[1]);
         return o;
     }
-    __device__ __forceinline__ static void store_cc(VC& c, const CC& o) { c.ni[0] = o.ni0; c.ni[1] = o.ni1; c.ti[0] = o.ti0; c.ti[1] = o.ti1; }
-    // b2ContactSolver::SolveVelocityConstraints for one contact (wave-uniform values)
-    __device__ __forceinline__ static void cc_update(CC& c, V2& vA, float& wA, V2& vB, float& wB) {
-        const float mA = c.mA, iA = c.iA, mB = c.mB, iB = c.iB;
-        const V2 normal = c.normal, tangent = c.tangent;
+    __device__ __forceinline__ static void store_cc(VC& c, const CC& o) { c.ni[0] = o.ni.x; c.ni[1] = o.ni.y; c.ti[0] = o.ti.x; c.ti[1] = o.ti.y; }
+    // b2ContactSolver::SolveVelocityConstraints for one contact, with the float operations and
+    // order of solver_velocity (each packed half is the scalar expression, see P2 in mrp_math.h).
+    // `pcount` is wave-uniform; `pick(c)` turns the block solver's per-lane case condition into the
+    // wave-uniform decision (uni: identical lanes; lane_bit: lane i's).  Reads the impulses from
+    // c.ni / c.ti and returns the new ones in ni / ti (the caller decides which lanes keep them).
+    template <class Pick>
+    __device__ __forceinline__ static void vel_update(const CC& c, int pcount, Pick pick, P2& ni, P2& ti,
+                                                          P2& vA, float& wA, P2& vB, float& wB) {
+        const P2 mA = c.mA, mB = c.mB;
+        const float iA = c.iA, iB = c.iB;
+        const P2 normal = c.normal, tangent = c.tangent;
+        ni = c.ni; ti = c.ti;
         {   // friction, point 0
-            V2 rA = v2(c.rAx0, c.rAy0), rB = v2(c.rBx0, c.rBy0);
-            V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
-            float vt = vdot(dv, tangent);
+            const P2 dv = ((vB + (pbc(wB) * c.rB0)) - vA) - (pbc(wA) * c.rA0);
+            const float vt = pdot(dv, tangent);
             float lambda = c.tmass0 * (-vt);
-            float maxFriction = c.friction * c.ni0;
-            float newImpulse = fclamp(c.ti0 + lambda, -maxFriction, maxFriction);
-            lambda = newImpulse - c.ti0;
-            c.ti0 = newImpulse;
-            V2 P = vmul(lambda, tangent);
-            vA = vsub(vA, vmul(mA, P));
-            wA -= iA * vcross(rA, P);
-            vB = vadd(vB, vmul(mB, P));
-            wB += iB * vcross(rB, P);
+            const float maxFriction = c.friction * ni.x;
+            const float newImpulse = fclamp(ti.x + lambda, -maxFriction, maxFriction);
+            lambda = newImpulse - ti.x;
+            ti.x = newImpulse;
+            const P2 P = pbc(lambda) * tangent;
+            vA = vA - mA * P;
+            wA -= iA * pcrossp(c.rA0, P);
+            vB = vB + mB * P;
+            wB += iB * pcrossp(c.rB0, P);
         }
-        if (c.pcount == 2) {   // friction, point 1
-            V2 rA = v2(c.rAx1, c.rAy1), rB = v2(c.rBx1, c.rBy1);
-            V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
-            float vt = vdot(dv, tangent);
+        if (pcount == 2) {   // friction, point 1
+            const P2 dv = ((vB + (pbc(wB) * c.rB1)) - vA) - (pbc(wA) * c.rA1);
+            const float vt = pdot(dv, tangent);
             float lambda = c.tmass1 * (-vt);
-            float maxFriction = c.friction * c.ni1;
-            float newImpulse = fclamp(c.ti1 + lambda, -maxFriction, maxFriction);
-            lambda = newImpulse - c.ti1;
-            c.ti1 = newImpulse;
-            V2 P = vmul(lambda, tangent);
-            vA = vsub(vA, vmul(mA, P));
-            wA -= iA * vcross(rA, P);
-            vB = vadd(vB, vmul(mB, P));
-            wB += iB * vcross(rB, P);
+            const float maxFriction = c.friction * ni.y;
+            const float newImpulse = fclamp(ti.y + lambda, -maxFriction, maxFriction);
+            lambda = newImpulse - ti.y;
+            ti.y = newImpulse;
+            const P2 P = pbc(lambda) * tangent;
+            vA = vA - mA * P;
+            wA -= iA * pcrossp(c.rA1, P);
+            vB = vB + mB * P;
+            wB += iB * pcrossp(c.rB1, P);
         }
-        if (c.pcount == 1) {
-            V2 rA = v2(c.rAx0, c.rAy0), rB = v2(c.rBx0, c.rBy0);
-            V2 dv = vsub(vsub(vadd(vB, vcross_sv(wB, rB)), vA), vcross_sv(wA, rA));
-            float vn = vdot(dv, normal);
-            float lambda = -c.nmass0 * (vn - c.vbias0);
-            float newImpulse = fmax_(c.ni0 + lambda, 0.0f);
-            lambda = newImpulse - c.ni0;
-            c.ni0 = newImpulse;
-            V2 P = vmul(lambda, normal);
-            vA = vsub(vA, vmul(mA, P));
-            wA -= iA * vcross(rA, P);
-            vB = vadd(vB, vmul(mB, P));
-            wB += iB * vcross(rB, P);
+        if (pcount == 1) {
+            const P2 dv = ((vB + (pbc(wB) * c.rB0)) - vA) - (pbc(wA) * c.rA0);
+            const float vn = pdot(dv, normal);
+            float lambda = -c.nmass0 * (vn - c.vbias.x);
+            const float newImpulse = fmax_(ni.x + lambda, 0.0f);
+            lambda = newImpulse - ni.x;
+            ni.x = newImpulse;
+            const P2 P = pbc(lambda) * normal;
+            vA = vA - mA * P;
+            wA -= iA * pcrossp(c.rA0, P);
+            vB = vB + mB * P;
+            wB += iB * pcrossp(c.rB0, P);
         } else {
-            const float k0 = c.k0, k1 = c.k1, k2 = c.k1, k3 = c.k3, nm0 = c.nm0, nm1 = c.nm1, nm2 = c.nm1, nm3 = c.nm3;
-            V2 r1A = v2(c.rAx0, c.rAy0), r1B = v2(c.rBx0, c.rBy0);
-            V2 r2A = v2(c.rAx1, c.rAy1), r2B = v2(c.rBx1, c.rBy1);
-            V2 a = v2(c.ni0, c.ni1);
-            V2 dv1 = vsub(vsub(vadd(vB, vcross_sv(wB, r1B)), vA), vcross_sv(wA, r1A));
-            V2 dv2 = vsub(vsub(vadd(vB, vcross_sv(wB, r2B)), vA), vcross_sv(wA, r2A));
-            float vn1 = vdot(dv1, normal), vn2 = vdot(dv2, normal);
-            V2 b = v2(vn1 - c.vbias0, vn2 - c.vbias1);
-            b = vsub(b, v2(k0 * a.x + k2 * a.y, k1 * a.x + k3 * a.y));
-            V2 x = vneg(v2(nm0 * b.x + nm2 * b.y, nm1 * b.x + nm3 * b.y));
+            const P2 a = ni;
+            const P2 dv1 = ((vB + (pbc(wB) * c.rB0)) - vA) - (pbc(wA) * c.rA0);
+            const P2 dv2 = ((vB + (pbc(wB) * c.rB1)) - vA) - (pbc(wA) * c.rA1);
+            float vn1 = pdot(dv1, normal), vn2 = pdot(dv2, normal);
+            // b = (vn1 - vbias0, vn2 - vbias1) - (k0*a.x + k2*a.y, k1*a.x + k3*a.y), k2 = k1
+            P2 b = p2(vn1, vn2) - c.vbias;
+            b = b - (c.k01 * pbc(a.x) + c.k13 * pbc(a.y));
+            // x = -(nm0*b.x + nm2*b.y, nm1*b.x + nm3*b.y), nm2 = nm1
+            P2 x = -(c.nm01 * pbc(b.x) + c.nm13 * pbc(b.y));
             bool ok = true;
-            if (!uni(x.x >= 0.0f && x.y >= 0.0f)) {
+            if (!pick(x.x >= 0.0f && x.y >= 0.0f)) {
                 x.x = -c.nmass0 * b.x; x.y = 0.0f;
-                vn2 = k1 * x.x + b.y;
-                if (!uni(x.x >= 0.0f && vn2 >= 0.0f)) {
+                vn2 = c.k01.y * x.x + b.y;
+                if (!pick(x.x >= 0.0f && vn2 >= 0.0f)) {
                     x.x = 0.0f; x.y = -c.nmass1 * b.y;
-                    vn1 = k2 * x.y + b.x;
-                    if (!uni(x.y >= 0.0f && vn1 >= 0.0f)) {
+                    vn1 = c.k01.y * x.y + b.x;
+                    if (!pick(x.y >= 0.0f && vn1 >= 0.0f)) {
                         x.x = 0.0f; x.y = 0.0f;
-                        ok = uni(b.x >= 0.0f && b.y >= 0.0f);
+                        ok = pick(b.x >= 0.0f && b.y >= 0.0f);
                     }
                 }
             }
             if (ok) {
-                V2 d = vsub(x, a);
-                V2 P1 = vmul(d.x, normal), P2 = vmul(d.y, normal);
-                vA = vsub(vA, vmul(mA, vadd(P1, P2)));
-                wA -= iA * (vcross(r1A, P1) + vcross(r2A, P2));
-                vB = vadd(vB, vmul(mB, vadd(P1, P2)));
-                wB += iB * (vcross(r1B, P1) + vcross(r2B, P2));
-                c.ni0 = x.x; c.ni1 = x.y;
+                const P2 d = x - a;
+                const P2 P1 = pbc(d.x) * normal, P2v = pbc(d.y) * normal;
+                const P2 S = P1 + P2v;
+                vA = vA - mA * S;
+                wA -= iA * (pcrossp(c.rA0, P1) + pcrossp(c.rA1, P2v));
+                vB = vB + mB * S;
+                wB += iB * (pcrossp(c.rB0, P1) + pcrossp(c.rB1, P2v));
+                ni = x;
             }
         }
+    }
+    // the register-resident form: identical lanes, every lane keeps the result
+    __device__ __forceinline__ static void cc_update(CC& c, P2& vA, float& wA, P2& vB, float& wB) {
+        P2 ni, ti;
+        vel_update(c, __builtin_amdgcn_readfirstlane(c.pcount), [](bool x) { return uni(x); }, ni, ti, vA, wA, vB, wB);
+        c.ni = ni; c.ti = ti;
     }
     // exact early exit (see solver_velocity_lanes): the state after sweep k is compared with the
     // snapshot of sweep k-2 at every sweep k with iters - k = 0 mod 4, the snapshot is taken at
     // iters - k = 2 mod 4; true = the remaining sweeps are no-ops.  The comparison is one OR-tree
     // of XORs of the bit patterns (wave-uniform values: any lane decides).
+    // The snapshot is held lane-distributed (value k in lane k of ONE register): the sweep state of
+    // the register-resident paths is wave-uniform, so lane k can stand for all of value k, and the
+    // snapshot costs one VGPR instead of NS (the sweeps' register peak sets k_step's spills).
     template <int NS> struct Snap {
-        float s[NS];
+        static_assert(NS <= 64, "one lane per snapshot value");
+        float s;
         bool have;
-        __device__ __forceinline__ void take(const float (&cur)[NS]) {
+        __device__ __forceinline__ static float gather(const float (&cur)[NS]) {
+            float v = cur[0];
 #pragma unroll
-            for (int k = 0; k < NS; ++k) s[k] = cur[k];
-            have = true;
+            for (int k = 1; k < NS; ++k) v = wrl(v, __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cur[k]))), k);
+            return v;
         }
+        __device__ __forceinline__ Snap(const float (&cur)[NS], bool h) : s(gather(cur)), have(h) {}
+        __device__ __forceinline__ void take(const float (&cur)[NS]) { s = gather(cur); have = true; }
         __device__ __forceinline__ bool same(const float (&cur)[NS]) const {
-            uint32_t d = 0u;
-#pragma unroll
-            for (int k = 0; k < NS; ++k) d |= __float_as_uint(cur[k]) ^ __float_as_uint(s[k]);
-            return have && uni(d == 0u);
+            const bool diff = (int)threadIdx.x < NS && __float_as_uint(gather(cur)) != __float_as_uint(s);
+            return have && __builtin_amdgcn_ballot_w64(diff) == 0;
         }
         // one early-exit point after sweep `it + 1` of `iters`
         __device__ __forceinline__ bool step(int it, int iters, const float (&cur)[NS]) {
@@ -1280,15 +1217,16 @@ template <int ENV> struct World {
     __device__ __forceinline__ int solver_velocity_one(Isl& is, VC* vcs, int iters, bool early_exit = true) {
         CC c = load_cc(vcs[0]);
         const int ia = vcs[0].iaI, ib = vcs[0].ibI;
-        V2 vA = v2(is.vvx[ia], is.vvy[ia]); float wA = is.vw[ia];
-        V2 vB = v2(is.vvx[ib], is.vvy[ib]); float wB = is.vw[ib];
-        Snap<10> snap = {{vA.x, vA.y, wA, vB.x, vB.y, wB, c.ni0, c.ni1, c.ti0, c.ti1}, snap_initial(iters)};
+        P2 vA = p2(is.vvx[ia], is.vvy[ia]); float wA = is.vw[ia];
+        P2 vB = p2(is.vvx[ib], is.vvy[ib]); float wB = is.vw[ib];
+        const float init[10] = {vA.x, vA.y, wA, vB.x, vB.y, wB, c.ni.x, c.ni.y, c.ti.x, c.ti.y};
+        Snap<10> snap(init, snap_initial(iters));
         int sweeps = 0;
         for (int it = 0; it < iters; ++it) {
             ++sweeps;
             cc_update(c, vA, wA, vB, wB);
             if (early_exit && ((iters - it - 1) & 1) == 0) {
-                const float cur[10] = {vA.x, vA.y, wA, vB.x, vB.y, wB, c.ni0, c.ni1, c.ti0, c.ti1};
+                const float cur[10] = {vA.x, vA.y, wA, vB.x, vB.y, wB, c.ni.x, c.ni.y, c.ti.x, c.ti.y};
                 if (snap.step(it, iters, cur)) break;
             }
         }
@@ -1305,18 +1243,19 @@ template <int ENV> struct World {
     template <bool XA0, bool XA1>
     __device__ __forceinline__ int sweep_two(Isl& is, VC* vcs, int iters, bool early_exit, int x, int y, int z) {
         CC c0 = load_cc(vcs[0]), c1 = load_cc(vcs[1]);
-        V2 vX = v2(is.vvx[x], is.vvy[x]), vY = v2(is.vvx[y], is.vvy[y]), vZ = v2(is.vvx[z], is.vvy[z]);
+        P2 vX = p2(is.vvx[x], is.vvy[x]), vY = p2(is.vvx[y], is.vvy[y]), vZ = p2(is.vvx[z], is.vvy[z]);
         float wX = is.vw[x], wY = is.vw[y], wZ = is.vw[z];
-        Snap<17> snap = {{vX.x, vX.y, wX, vY.x, vY.y, wY, vZ.x, vZ.y, wZ, c0.ni0, c0.ni1, c0.ti0, c0.ti1,
-                          c1.ni0, c1.ni1, c1.ti0, c1.ti1}, snap_initial(iters)};
+        const float init[17] = {vX.x, vX.y, wX, vY.x, vY.y, wY, vZ.x, vZ.y, wZ, c0.ni.x, c0.ni.y, c0.ti.x, c0.ti.y,
+                                c1.ni.x, c1.ni.y, c1.ti.x, c1.ti.y};
+        Snap<17> snap(init, snap_initial(iters));
         int sweeps = 0;
         for (int it = 0; it < iters; ++it) {
             ++sweeps;
             if (XA0) cc_update(c0, vX, wX, vY, wY); else cc_update(c0, vY, wY, vX, wX);
             if (XA1) cc_update(c1, vX, wX, vZ, wZ); else cc_update(c1, vZ, wZ, vX, wX);
             if (early_exit && ((iters - it - 1) & 1) == 0) {
-                const float cur[17] = {vX.x, vX.y, wX, vY.x, vY.y, wY, vZ.x, vZ.y, wZ, c0.ni0, c0.ni1, c0.ti0, c0.ti1,
-                                       c1.ni0, c1.ni1, c1.ti0, c1.ti1};
+                const float cur[17] = {vX.x, vX.y, wX, vY.x, vY.y, wY, vZ.x, vZ.y, wZ, c0.ni.x, c0.ni.y, c0.ti.x, c0.ti.y,
+                                       c1.ni.x, c1.ni.y, c1.ti.x, c1.ti.y};
                 if (snap.step(it, iters, cur)) break;
             }
         }
@@ -1333,17 +1272,17 @@ template <int ENV> struct World {
     template <bool SAME>
     __device__ __forceinline__ int sweep_same(Isl& is, VC* vcs, int iters, bool early_exit, int p, int q) {
         CC c0 = load_cc(vcs[0]), c1 = load_cc(vcs[1]);
-        V2 vP = v2(is.vvx[p], is.vvy[p]), vQ = v2(is.vvx[q], is.vvy[q]);
+        P2 vP = p2(is.vvx[p], is.vvy[p]), vQ = p2(is.vvx[q], is.vvy[q]);
         float wP = is.vw[p], wQ = is.vw[q];
-        Snap<14> snap = {{vP.x, vP.y, wP, vQ.x, vQ.y, wQ, c0.ni0, c0.ni1, c0.ti0, c0.ti1, c1.ni0, c1.ni1, c1.ti0, c1.ti1},
-                         snap_initial(iters)};
+        const float init[14] = {vP.x, vP.y, wP, vQ.x, vQ.y, wQ, c0.ni.x, c0.ni.y, c0.ti.x, c0.ti.y, c1.ni.x, c1.ni.y, c1.ti.x, c1.ti.y};
+        Snap<14> snap(init, snap_initial(iters));
         int sweeps = 0;
         for (int it = 0; it < iters; ++it) {
             ++sweeps;
             cc_update(c0, vP, wP, vQ, wQ);
             if (SAME) cc_update(c1, vP, wP, vQ, wQ); else cc_update(c1, vQ, wQ, vP, wP);
             if (early_exit && ((iters - it - 1) & 1) == 0) {
-                const float cur[14] = {vP.x, vP.y, wP, vQ.x, vQ.y, wQ, c0.ni0, c0.ni1, c0.ti0, c0.ti1, c1.ni0, c1.ni1, c1.ti0, c1.ti1};
+                const float cur[14] = {vP.x, vP.y, wP, vQ.x, vQ.y, wQ, c0.ni.x, c0.ni.y, c0.ti.x, c0.ti.y, c1.ni.x, c1.ni.y, c1.ti.x, c1.ti.y};
                 if (snap.step(it, iters, cur)) break;
             }
         }
