@@ -1315,15 +1315,18 @@ template <int ENV> struct World {
     // keyed by the angle's bit pattern (b2Rot::Set is a pure function of the angle, and a body
     // with invI = 0 - the v0 agents, the walls - keeps its angle through every pass).  Returns
     // the number of passes run (the reference's loop count).  Every thread calls it; nc <= 64.
+    // Rotations as packed (c, s) pairs: pmul_rv(q, v) = q * v.x + pperp(q) * v.y (see P2).
+    __device__ __forceinline__ static P2 rot_cs(float angle) { const Rot q = rot(angle); return p2(q.c, q.s); }
+    __device__ __forceinline__ static P2 prot(P2 q, P2 v) { return q * pbc(v.x) + pperp(q) * pbc(v.y); }
     struct RotMemo {
         uint32_t k0 = 0u, k1 = 0u;   // +0.0f: b2Rot::Set(+0) = {+0, 1}
-        Rot q0 = {0.0f, 1.0f}, q1 = {0.0f, 1.0f};
+        P2 q0 = {1.0f, 0.0f}, q1 = {1.0f, 0.0f};
         bool next1 = false;
-        __device__ __forceinline__ Rot get(float angle) {
+        __device__ __forceinline__ P2 get(float angle) {
             const uint32_t b = __float_as_uint(angle);
             if (b == k0) return q0;
             if (b == k1) return q1;
-            const Rot q = rot(angle);
+            const P2 q = rot_cs(angle);
             if (next1) { k1 = b; q1 = q; } else { k0 = b; q0 = q; }
             next1 = !next1;
             return q;
@@ -1335,74 +1338,86 @@ template <int ENV> struct World {
     // through readlane / writelane.  Same float operations in the same order as solver_position.
     struct UniMemo {   // RotMemo with wave-uniform (identical-lane) angles: scalar branches
         uint32_t k0 = 0u, k1 = 0u;
-        Rot q0 = {0.0f, 1.0f}, q1 = {0.0f, 1.0f};
+        P2 q0 = {1.0f, 0.0f}, q1 = {1.0f, 0.0f};
         bool next1 = false;
-        __device__ __forceinline__ Rot get(float angle) {
+        __device__ __forceinline__ P2 get(float angle) {
             const uint32_t b = __float_as_uint(angle);
             if (uni(b == k0)) return q0;
             if (uni(b == k1)) return q1;
-            const Rot q = rot(angle);
+            const P2 q = rot_cs(angle);
             if (next1) { k1 = b; q1 = q; } else { k0 = b; q0 = q; }
             next1 = !next1;
             return q;
         }
     };
-    struct PCC {   // one contact's position-constraint constants (PC + masses), in registers
-        float lcAx, lcAy, lcBx, lcBy, lnx, lny, lpx0, lpy0, qx0, qy0, qx1, qy1, radA, radB, mA, iA, mB, iB;
+    struct PCC {   // one contact's position-constraint constants (PC + masses), in registers, packed
+        P2 lcA, lcB, ln, lp0, q0, q1;   // local centres, local normal, local plane point, local points 0 / 1
+        P2 mA, mB;                      // (mA, mA), (mB, mB)
+        float radA, radB, iA, iB;
         int pcount, type;
     };
     __device__ __forceinline__ static PCC load_pcc(const VC& vc, const PC& pc, bool toi, int toiA, int toiB) {
         PCC o;
-        o.lcAx = pc.lcAx; o.lcAy = pc.lcAy; o.lcBx = pc.lcBx; o.lcBy = pc.lcBy;
-        o.lnx = pc.lnx; o.lny = pc.lny; o.lpx0 = pc.lpx0; o.lpy0 = pc.lpy0;
-        o.qx0 = pc.lpx[0]; o.qy0 = pc.lpy[0]; o.qx1 = pc.lpx[1]; o.qy1 = pc.lpy[1];
+        o.lcA = p2(pc.lcAx, pc.lcAy); o.lcB = p2(pc.lcBx, pc.lcBy);
+        o.ln = p2(pc.lnx, pc.lny); o.lp0 = p2(pc.lpx0, pc.lpy0);
+        o.q0 = p2(pc.lpx[0], pc.lpy[0]); o.q1 = p2(pc.lpx[1], pc.lpy[1]);
         o.radA = pc.rA; o.radB = pc.rB;
-        o.mA = vc.mA; o.iA = vc.iA; o.mB = vc.mB; o.iB = vc.iB;
+        float mA = vc.mA, iA = vc.iA, mB = vc.mB, iB = vc.iB;
         if (toi) {
-            if (!(vc.iaI == toiA || vc.iaI == toiB)) { o.mA = 0.0f; o.iA = 0.0f; }
-            if (!(vc.ibI == toiA || vc.ibI == toiB)) { o.mB = 0.0f; o.iB = 0.0f; }
+            if (!(vc.iaI == toiA || vc.iaI == toiB)) { mA = 0.0f; iA = 0.0f; }
+            if (!(vc.ibI == toiA || vc.ibI == toiB)) { mB = 0.0f; iB = 0.0f; }
         }
-        o.pcount = __builtin_amdgcn_readfirstlane(pc.pointCount);
-        o.type = __builtin_amdgcn_readfirstlane(pc.type);
+        o.mA = pbc(mA); o.iA = iA; o.mB = pbc(mB); o.iB = iB;
+        o.pcount = pc.pointCount;
+        o.type = pc.type;
         return o;
     }
-    // b2ContactSolver::SolvePositionConstraints for one contact (wave-uniform values)
-    __device__ __forceinline__ static void pcc_update(const PCC& c, V2& cA, float& aA, V2& cB, float& aB, float& minSep,
-                                                      float baum, UniMemo& memo) {
+    // b2ContactSolver::SolvePositionConstraints (SolveTOIPositionConstraints) for one contact, with
+    // the float operations and order of solver_position (each packed half is the scalar
+    // expression).  `getA` / `getB` give the rotation of an angle, called A then B per point as
+    // the reference sets xfA.q then xfB.q; `onSep(sep)` sees each point's separation.
+    template <class GetA, class GetB, class OnSep>
+    __device__ __forceinline__ static void pos_update(const PCC& c, int pcount, int type, float baum, GetA getA, GetB getB,
+                                                      OnSep onSep, P2& cA, float& aA, P2& cB, float& aB) {
         for (int j = 0; j < 2; ++j) {
-            if (j == c.pcount) break;
-            Xf xA, xB;
-            xA.q = memo.get(aA); xB.q = memo.get(aB);
-            xA.p = vsub(cA, mul_rv(xA.q, v2(c.lcAx, c.lcAy)));
-            xB.p = vsub(cB, mul_rv(xB.q, v2(c.lcBx, c.lcBy)));
-            const V2 lp = j == 0 ? v2(c.qx0, c.qy0) : v2(c.qx1, c.qy1);
-            V2 normal, point; float sep;
-            if (c.type == MT_FACEA) {
-                normal = mul_rv(xA.q, v2(c.lnx, c.lny));
-                V2 planePoint = mul_xv(xA, v2(c.lpx0, c.lpy0));
-                V2 clipPoint = mul_xv(xB, lp);
-                sep = vdot(vsub(clipPoint, planePoint), normal) - c.radA - c.radB;
+            if (j == pcount) break;
+            const P2 qA = getA(aA), qB = getB(aB);
+            const P2 pA = cA - prot(qA, c.lcA), pB = cB - prot(qB, c.lcB);
+            const P2 lp = j == 0 ? c.q0 : c.q1;
+            P2 normal, point; float sep;
+            if (type == MT_FACEA) {
+                normal = prot(qA, c.ln);
+                const P2 planePoint = prot(qA, c.lp0) + pA;
+                const P2 clipPoint = prot(qB, lp) + pB;
+                sep = pdot(clipPoint - planePoint, normal) - c.radA - c.radB;
                 point = clipPoint;
             } else {
-                normal = mul_rv(xB.q, v2(c.lnx, c.lny));
-                V2 planePoint = mul_xv(xB, v2(c.lpx0, c.lpy0));
-                V2 clipPoint = mul_xv(xA, lp);
-                sep = vdot(vsub(clipPoint, planePoint), normal) - c.radA - c.radB;
+                normal = prot(qB, c.ln);
+                const P2 planePoint = prot(qB, c.lp0) + pB;
+                const P2 clipPoint = prot(qA, lp) + pA;
+                sep = pdot(clipPoint - planePoint, normal) - c.radA - c.radB;
                 point = clipPoint;
-                normal = vneg(normal);
+                normal = -normal;
             }
-            V2 rA = vsub(point, cA), rB = vsub(point, cB);
-            minSep = fmin_(minSep, sep);
-            float Cc = fclamp(baum * (sep + LINEAR_SLOP), -MAX_LINEAR_CORRECTION, 0.0f);
-            float rnA = vcross(rA, normal), rnB = vcross(rB, normal);
-            float K = c.mA + c.mB + c.iA * rnA * rnA + c.iB * rnB * rnB;
-            float impulse = K > 0.0f ? -Cc / K : 0.0f;
-            V2 Pv = vmul(impulse, normal);
-            cA = vsub(cA, vmul(c.mA, Pv));
-            aA -= c.iA * vcross(rA, Pv);
-            cB = vadd(cB, vmul(c.mB, Pv));
-            aB += c.iB * vcross(rB, Pv);
+            const P2 rA = point - cA, rB = point - cB;
+            onSep(sep);
+            const float Cc = fclamp(baum * (sep + LINEAR_SLOP), -MAX_LINEAR_CORRECTION, 0.0f);
+            const float rnA = pcross(rA, normal), rnB = pcross(rB, normal);
+            const float K = c.mA.x + c.mB.x + c.iA * rnA * rnA + c.iB * rnB * rnB;
+            const float impulse = K > 0.0f ? -Cc / K : 0.0f;
+            const P2 Pv = pbc(impulse) * normal;
+            cA = cA - c.mA * Pv;
+            aA -= c.iA * pcross(rA, Pv);
+            cB = cB + c.mB * Pv;
+            aB += c.iB * pcross(rB, Pv);
         }
+    }
+    // the register-resident form: identical lanes, one wave-uniform memo
+    __device__ __forceinline__ static void pcc_update(const PCC& c, P2& cA, float& aA, P2& cB, float& aB, float& minSep,
+                                                      float baum, UniMemo& memo) {
+        auto get = [&memo](float a) { return memo.get(a); };
+        pos_update(c, __builtin_amdgcn_readfirstlane(c.pcount), __builtin_amdgcn_readfirstlane(c.type), baum, get, get,
+                   [&minSep](float sep) { minSep = fmin_(minSep, sep); }, cA, aA, cB, aB);
     }
     // NC = 1: contact 0 on (P, Q).  NC = 2: SAMEB - both contacts on P, Q (contact 1 as (P, Q) if
     // XA1 else (Q, P)); otherwise X (= P) shared, Y (= Q) the other body of contact 0, Z of contact 1,
@@ -1412,7 +1427,7 @@ template <int ENV> struct World {
                                              int p, int q, int z) {
         const PCC c0 = load_pcc(vcs[0], pcs[0], toi, toiA, toiB);
         const PCC c1 = load_pcc(vcs[NC - 1], pcs[NC - 1], toi, toiA, toiB);
-        V2 cP = v2(is.pcx[p], is.pcy[p]), cQ = v2(is.pcx[q], is.pcy[q]), cZ = v2(is.pcx[z], is.pcy[z]);
+        P2 cP = p2(is.pcx[p], is.pcy[p]), cQ = p2(is.pcx[q], is.pcy[q]), cZ = p2(is.pcx[z], is.pcy[z]);
         float aP = is.pa[p], aQ = is.pa[q], aZ = is.pa[z];
         const float baum = toi ? TOI_BAUMGARTE : BAUMGARTE;
         const float exitSep = toi ? -1.5f * LINEAR_SLOP : -3.0f * LINEAR_SLOP;
@@ -1457,17 +1472,8 @@ template <int ENV> struct World {
     __device__ __forceinline__ int solver_position_lanes(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB, int iters) {
         const int nc = is.nc;
         const int me = tid < nc ? tid : 0;   // lanes >= nc evaluate a copy of contact 0 and are never kept
-        const VC& vc = vcs[me];
-        const PC& pc = pcs[me];
-        const int cia = vc.iaI, cib = vc.ibI, cpc = pc.pointCount, ctype = pc.type;
-        float mA = vc.mA, iA = vc.iA, mB = vc.mB, iB = vc.iB;
-        if (toi) {
-            if (!(cia == toiA || cia == toiB)) { mA = 0.0f; iA = 0.0f; }
-            if (!(cib == toiA || cib == toiB)) { mB = 0.0f; iB = 0.0f; }
-        }
-        const float lcAx = pc.lcAx, lcAy = pc.lcAy, lcBx = pc.lcBx, lcBy = pc.lcBy;
-        const float lnx = pc.lnx, lny = pc.lny, lpx0 = pc.lpx0, lpy0 = pc.lpy0, radA = pc.rA, radB = pc.rB;
-        const float qx0 = pc.lpx[0], qy0 = pc.lpy[0], qx1 = pc.lpx[1], qy1 = pc.lpy[1];
+        const PCC my = load_pcc(vcs[me], pcs[me], toi, toiA, toiB);
+        const int cia = vcs[me].iaI, cib = vcs[me].ibI;
         const int bk = tid < is.nb ? tid : 0;
         float bx = is.pcx[bk], by = is.pcy[bk], ba = is.pa[bk];
         const float baum = toi ? TOI_BAUMGARTE : BAUMGARTE;
@@ -1479,43 +1485,14 @@ template <int ENV> struct World {
             ++it;
             float minSep = 0.0f;   // wave-uniform: lane i's separations in contact/point order
             for (int i = 0; i < ncu; ++i) {
-                const int ia = rdli(cia, i), ib = rdli(cib, i), pcount = rdli(cpc, i), type = rdli(ctype, i);
-                V2 cA = v2(rdl(bx, ia), rdl(by, ia)); float aA = rdl(ba, ia);
-                V2 cB = v2(rdl(bx, ib), rdl(by, ib)); float aB = rdl(ba, ib);
-                for (int j = 0; j < 2; ++j) {
-                    if (j == pcount) break;
-                    Xf xA, xB;
-                    xA.q = memo.get(rdl(aA, i)); xB.q = memo.get(rdl(aB, i));
-                    xA.p = vsub(cA, mul_rv(xA.q, v2(lcAx, lcAy)));
-                    xB.p = vsub(cB, mul_rv(xB.q, v2(lcBx, lcBy)));
-                    const V2 lp = j == 0 ? v2(qx0, qy0) : v2(qx1, qy1);
-                    V2 normal, point; float sep;
-                    if (type == MT_FACEA) {
-                        normal = mul_rv(xA.q, v2(lnx, lny));
-                        V2 planePoint = mul_xv(xA, v2(lpx0, lpy0));
-                        V2 clipPoint = mul_xv(xB, lp);
-                        sep = vdot(vsub(clipPoint, planePoint), normal) - radA - radB;
-                        point = clipPoint;
-                    } else {
-                        normal = mul_rv(xB.q, v2(lnx, lny));
-                        V2 planePoint = mul_xv(xB, v2(lpx0, lpy0));
-                        V2 clipPoint = mul_xv(xA, lp);
-                        sep = vdot(vsub(clipPoint, planePoint), normal) - radA - radB;
-                        point = clipPoint;
-                        normal = vneg(normal);
-                    }
-                    V2 rA = vsub(point, cA), rB = vsub(point, cB);
-                    minSep = fmin_(minSep, rdl(sep, i));
-                    float Cc = fclamp(baum * (sep + LINEAR_SLOP), -MAX_LINEAR_CORRECTION, 0.0f);
-                    float rnA = vcross(rA, normal), rnB = vcross(rB, normal);
-                    float K = mA + mB + iA * rnA * rnA + iB * rnB * rnB;
-                    float impulse = K > 0.0f ? -Cc / K : 0.0f;
-                    V2 Pv = vmul(impulse, normal);
-                    cA = vsub(cA, vmul(mA, Pv));
-                    aA -= iA * vcross(rA, Pv);
-                    cB = vadd(cB, vmul(mB, Pv));
-                    aB += iB * vcross(rB, Pv);
-                }
+                const int ia = rdli(cia, i), ib = rdli(cib, i), pcount = rdli(my.pcount, i), type = rdli(my.type, i);
+                P2 cA = p2(rdl(bx, ia), rdl(by, ia)); float aA = rdl(ba, ia);
+                P2 cB = p2(rdl(bx, ib), rdl(by, ib)); float aB = rdl(ba, ib);
+                // every lane evaluates ITS contact's point updates; the rotations are those of lane
+                // i's angles (wave-uniform), and lane i's result is kept
+                auto get = [&memo, i](float a) { return memo.get(rdl(a, i)); };
+                pos_update(my, pcount, type, baum, get, get, [&minSep, i](float sep) { minSep = fmin_(minSep, rdl(sep, i)); },
+                           cA, aA, cB, aB);
                 bx = wrl(bx, rdl(cA.x, i), ia); by = wrl(by, rdl(cA.y, i), ia); ba = wrl(ba, rdl(aA, i), ia);
                 bx = wrl(bx, rdl(cB.x, i), ib); by = wrl(by, rdl(cB.y, i), ib); ba = wrl(ba, rdl(aB, i), ib);
             }
