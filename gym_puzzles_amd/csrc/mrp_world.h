@@ -1067,7 +1067,7 @@ template <int ENV> struct World {
     // v_pk_* instruction for both halves of a b2Vec2 operation) and the impulses (the state).
     struct CC {
         P2 rA0, rB0, rA1, rB1;   // arms of points 0 and 1, stored as pperp(r) = (-r.y, r.x) (see pcrossp)
-        P2 normal, tangent, vbias, k01, k13, nm01, nm13;   // K = [k0 k1; k1 k3], K^-1 = [nm0 nm1; nm1 nm3]
+        P2 normal, vbias, k01, k13, nm01, nm13;   // K = [k0 k1; k1 k3], K^-1 = [nm0 nm1; nm1 nm3]
         P2 mA, mB;   // (mA, mA), (mB, mB): broadcast once, not re-splatted (and hoisted into extra pairs) per use
         float nmass0, nmass1, tmass0, tmass1, iA, iB, friction;
         int pcount;
@@ -1078,8 +1078,6 @@ template <int ENV> struct World {
         o.rA0 = p2(-c.rAy[0], c.rAx[0]); o.rB0 = p2(-c.rBy[0], c.rBx[0]);
         o.rA1 = p2(-c.rAy[1], c.rAx[1]); o.rB1 = p2(-c.rBy[1], c.rBx[1]);
         o.normal = p2(c.nx, c.ny);
-        const V2 t = vcross_vs(v2(c.nx, c.ny), 1.0f);
-        o.tangent = p2(t.x, t.y);
         o.vbias = p2(c.vbias[0], c.vbias[1]);
         o.k01 = p2(c.k0, c.k1); o.k13 = p2(c.k1, c.k3); o.nm01 = p2(c.nm0, c.nm1); o.nm13 = p2(c.nm1, c.nm3);
         o.nmass0 = c.nmass[0]; o.nmass1 = c.nmass[1]; o.tmass0 = c.tmass[0]; o.tmass1 = c.tmass[1];
@@ -1099,7 +1097,9 @@ template <int ENV> struct World {
                                                           P2& vA, float& wA, P2& vB, float& wB) {
         const P2 mA = c.mA, mB = c.mB;
         const float iA = c.iA, iB = c.iB;
-        const P2 normal = c.normal, tangent = c.tangent;
+        // tangent = b2Cross(normal, 1.0f) = (1*n.y, -1*n.x) = (n.y, -n.x) exactly: a half swap and a
+        // negation, which fold into the packed instructions' op_sel / neg modifiers
+        const P2 normal = c.normal, tangent = p2(normal.y, -normal.x);
         ni = c.ni; ti = c.ti;
         {   // friction, point 0
             const P2 dv = ((vB + (pbc(wB) * c.rB0)) - vA) - (pbc(wA) * c.rA0);
@@ -1178,6 +1178,10 @@ template <int ENV> struct World {
     }
     // the register-resident form: identical lanes, every lane keeps the result
     __device__ __forceinline__ static void cc_update(CC& c, P2& vA, float& wA, P2& vB, float& wB) {
+        // opaque to the optimiser once per update, so values derived from the normal (the tangent,
+        // its swapped / negated forms) are formed inside the instructions rather than hoisted out
+        // of the sweep loop into registers of their own
+        asm volatile("" : "+v"(c.normal));
         P2 ni, ti;
         vel_update(c, __builtin_amdgcn_readfirstlane(c.pcount), [](bool x) { return uni(x); }, ni, ti, vA, wA, vB, wB);
         c.ni = ni; c.ti = ti;
