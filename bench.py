@@ -77,6 +77,8 @@ def main():
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the per-step gather to rank 0")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--schedule", type=int, default=0, help="mrp_set_schedule mode: 1 costliest-first dispatch, 2 cost priority, 3 both")
+    ap.add_argument("--time-every", type=int, default=1,
+                    help="bracket every N-th timed step's launch with HIP events for kernel_ms (1 = every step)")
     ap.add_argument("--later-window", type=int, default=200,
                     help="diagnostic: also time this many steps starting near --later-start (0 = off; N=1 only)")
     ap.add_argument("--later-start", type=int, default=500)
@@ -146,16 +148,21 @@ def main():
     torch.cuda.synchronize(dev)
 
     K = args.steps
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    # HIP events bracket every `time_every`-th step's launch (a marker between two launches costs
+    # the stream a few microseconds; kernel_ms is the mean over the bracketed launches)
+    TE = max(1, args.time_every)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if k % TE == 0 else None for k in range(K)]
     if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(K):
-        ev[k][0].record(stream)
+        if ev[k] is not None:
+            ev[k][0].record(stream)
         b.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), trunc.data_ptr(), 0,
                       0 if norm is None else term.data_ptr())
-        ev[k][1].record(stream)
+        if ev[k] is not None:
+            ev[k][1].record(stream)
         if norm is not None:
             norm.step(obs, rew, done, nobs, nrew, term, nterm, epr, epl)
         if gather is not None:
@@ -164,6 +171,7 @@ def main():
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ev = [x for x in ev if x is not None]
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
     if distributed:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
