@@ -77,8 +77,8 @@ def main():
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the per-step gather to rank 0")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--schedule", type=int, default=0, help="mrp_set_schedule mode: 1 costliest-first dispatch, 2 cost priority, 3 both")
-    ap.add_argument("--time-every", type=int, default=1,
-                    help="bracket every N-th timed step's launch with HIP events for kernel_ms (1 = every step)")
+    ap.add_argument("--time-every", type=int, default=4,
+                    help="bracket every N-th timed step's launch with HIP events for kernel_ms (1 = every step; each marker pair costs the stream ~8 us)")
     ap.add_argument("--later-window", type=int, default=200,
                     help="diagnostic: also time this many steps starting near --later-start (0 = off; N=1 only)")
     ap.add_argument("--later-start", type=int, default=500)
@@ -240,6 +240,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
                          "kernel": "k_step", "kernel_ms": kern_ms,
+                         "kernel_ms_timing": f"HIP events around every {TE}th timed launch ({len(ev)} launches)",
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "limiter": "latency: the serial Gauss-Seidel chains (velocity sweeps, position passes, TOI) of "
                                     "the slowest lanes, one wave's VALU issue; not HBM and not MFMA",
