@@ -35,21 +35,84 @@ ALGO_BYTES = {0: 1657, 1: 3547, 2: 3613, 3: 3613, 4: 6085, 5: 1653, 6: 1653}   #
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 
 
-def cpu_baseline(env_id: int, lanes: int, seed: int, target_s: float = 20.0) -> dict:
+def host_cpus() -> dict:
+    """The host CPUs this process may use: nproc, the affinity mask, the cgroup CPU quota and
+    OMP_NUM_THREADS, and the resulting allotment.  On the GPU box `nproc` and the affinity mask
+    show the whole machine while the job's share is smaller, so the allotment is the cgroup quota
+    when one is set, else OMP_NUM_THREADS when the launcher set it, else the affinity mask."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                parts = f.read().split()
+            if path.endswith("cpu.max") and parts and parts[0] != "max":
+                quota = float(parts[0]) / float(parts[1])
+            elif path.endswith("quota_us") and parts and int(parts[0]) > 0:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                    quota = int(parts[0]) / float(f.read().split()[0])
+            if quota:
+                break
+        except (OSError, ValueError, IndexError):
+            continue
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    if quota:
+        allot, rule = max(1, min(aff, int(quota + 0.5))), "cgroup cpu quota"
+    elif omp:
+        allot, rule = max(1, min(aff, omp)), "OMP_NUM_THREADS (no cgroup quota)"
+    else:
+        allot, rule = aff, "affinity mask (no cgroup quota, no OMP_NUM_THREADS)"
+    return {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota, "omp_num_threads": omp,
+            "allotted": allot, "rule": rule}
+
+
+def cpu_baseline(env_id: int, lanes: int, seed: int, target_s: float = 15.0, single_s: float = 4.0) -> dict:
     """Time the CPU oracle (plain-C restatement, OpenMP over lanes) on a bounded sample of the
     same workload: same env, same lane count, same counter-RNG actions/spawns and auto-reset as
-    the GPU run, for as many steps as fit in about `target_s` seconds of wall time."""
+    the GPU run, on all allotted host cores, for as many steps as fit in about `target_s` seconds;
+    then one lane on one core (BASELINE.json configs[0]) for about `single_s` seconds."""
     from gym_puzzles_amd.spawn import draw_bounds
     from oracle.oracle import batch_run  # test infrastructure: baseline leg only
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)))
+    cpus = host_cpus()
+    threads = cpus["allotted"]
     bounds = draw_bounds(env_id)
     n, dt = batch_run(env_id, min(lanes, 32 * threads), 20, seed, bounds, threads=threads)    # calibrate
     rate = n / max(dt, 1e-6)
     steps = int(max(20, min(20000, target_s * rate / lanes)))
     n, dt = batch_run(env_id, lanes, steps, seed, bounds, threads=threads)
+    n1, dt1 = batch_run(env_id, 1, 200, seed, bounds, threads=1)
+    steps1 = int(max(200, min(200000, single_s * n1 / max(dt1, 1e-6))))
+    n1, dt1 = batch_run(env_id, 1, steps1, seed, bounds, threads=1)
     return {"value": n / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"{ENV_NAMES[env_id]}: {lanes} lanes x {steps} steps (device-RNG actions and spawns, "
-                      f"auto-reset) of the C oracle (oracle/), {threads} OpenMP threads, {dt:.1f} s"}
+                      f"auto-reset) of the C oracle (oracle/), {threads} OpenMP threads, {dt:.1f} s",
+            "host_cpus": cpus,
+            "single_lane_1core": {"value": n1 / dt1, "unit": "env-steps/s", "cores": 1,
+                                  "sample": f"1 lane x {steps1} steps of the same workload, 1 thread, {dt1:.1f} s "
+                                            "(BASELINE.json configs[0]: 1 env on the CPU)"}}
+
+
+def single_env_rate(env_name: str, steps: int = 300) -> dict:
+    """Diagnostic (never `value`): the gym-style drop-in path, `make(id)` then env.step(a) with host
+    numpy actions - one lane per call, PCIe round trip included (what train.py's DummyVecEnv drives)."""
+    from gym_puzzles_amd import make
+    env = make(env_name)
+    env.reset()
+    rs = np.random.RandomState(0)
+    acts = rs.uniform(-1, 1, size=(steps + 20, env.action_space.shape[0])).astype(np.float32)
+    for k in range(20):
+        _, _, d, _ = env.step(acts[k])
+        if d:
+            env.reset()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        _, _, d, _ = env.step(acts[20 + k])
+        if d:
+            env.reset()
+    dt = time.perf_counter() - t0
+    env.close()
+    return {"env_steps_per_s": steps / dt, "us_per_step": dt / steps * 1e6, "steps": steps,
+            "path": f"gym_puzzles_amd.make('{env_name}').step(): 1-lane kernel + host copies per call"}
 
 
 def load_traffic(env_id: int, lanes: int):
@@ -77,13 +140,21 @@ def main():
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the per-step gather to rank 0")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--schedule", type=int, default=0, help="mrp_set_schedule mode: 1 costliest-first dispatch, 2 cost priority, 3 both")
-    ap.add_argument("--time-every", type=int, default=4,
-                    help="bracket every N-th timed step's launch with HIP events for kernel_ms (1 = every step; each marker pair costs the stream ~8 us)")
+    ap.add_argument("--time-every", type=int, default=0,
+                    help="0 (default): one HIP event pair around all K timed launches on the kernel's stream, kernel_ms = "
+                         "that time / K; N >= 1: also bracket every N-th launch (per-launch spread; each marker pair "
+                         "costs the stream ~8 us, so this lowers `value`)")
+    ap.add_argument("--single-env", type=int, default=300,
+                    help="diagnostic: steps of the gym-style 1-lane make(id).step() path to time (0 = off; N=1 only)")
     ap.add_argument("--later-window", type=int, default=200,
                     help="diagnostic: also time this many steps starting near --later-start (0 = off; N=1 only)")
     ap.add_argument("--later-start", type=int, default=500)
     ap.add_argument("--episode", type=int, default=1,
                     help="diagnostic: also time one whole episode (TimeLimit steps from spawn, N=1 only; 0 = off)")
+    ap.add_argument("--multi-step", type=int, default=10,
+                    help="diagnostic: also time launches of K env steps (mrp_step_n_device) against single-step launches "
+                         "over the same window (0/1 = off; N=1 only)")
+    ap.add_argument("--multi-window", type=int, default=200, help="steps timed by the --multi-step diagnostic")
     ap.add_argument("--vecnormalize", action="store_true",
                     help="also run SB3 VecNormalize + Monitor statistics on the device every step (train.py:68,80-82)")
     args = ap.parse_args()
@@ -122,6 +193,7 @@ def main():
     rew = torch.zeros(L, dtype=torch.float32, device=dev)
     done = torch.zeros(L, dtype=torch.uint8, device=dev)
     trunc = torch.zeros(L, dtype=torch.uint8, device=dev)
+    status = torch.zeros(L, dtype=torch.uint8, device=dev)
     # one contiguous buffer per rank for the gather: [obs | reward | done] as float32
     gather = StepGather(Shard(rank, world, L), O, dev) if distributed and not args.no_gather else None
 
@@ -136,7 +208,7 @@ def main():
         norm.reset(torch.from_numpy(b.obs).to(dev), nobs)
 
     def one_step():
-        b.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), trunc.data_ptr(), 0,
+        b.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), trunc.data_ptr(), status.data_ptr(),
                       0 if norm is None else term.data_ptr())
         if norm is not None:
             norm.step(obs, rew, done, nobs, nrew, term, nterm, epr, epl)
@@ -148,18 +220,25 @@ def main():
     torch.cuda.synchronize(dev)
 
     K = args.steps
-    # HIP events bracket every `time_every`-th step's launch (a marker between two launches costs
-    # the stream a few microseconds; kernel_ms is the mean over the bracketed launches)
-    TE = max(1, args.time_every)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if k % TE == 0 else None for k in range(K)]
+    # kernel_ms: k_step's mean launch duration over exactly the K timed launches.  When k_step is
+    # the only work on the stream (no gather, no VecNormalize), one event pair around the K
+    # launches gives it without markers between launches (stream-busy time / K, launch gaps
+    # included, so kernel_ms <= ms_per_step); otherwise every launch is bracketed.  --time-every N
+    # adds per-launch brackets on every N-th launch for the spread (diagnostic; costs `value`).
+    alone = gather is None and norm is None
+    TE = args.time_every if alone else 1
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if TE and k % TE == 0 else None
+          for k in range(K)]
+    r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    r0.record(stream)
     for k in range(K):
         if ev[k] is not None:
             ev[k][0].record(stream)
-        b.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), trunc.data_ptr(), 0,
+        b.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), trunc.data_ptr(), status.data_ptr(),
                       0 if norm is None else term.data_ptr())
         if ev[k] is not None:
             ev[k][1].record(stream)
@@ -167,22 +246,41 @@ def main():
             norm.step(obs, rew, done, nobs, nrew, term, nterm, epr, epl)
         if gather is not None:
             gather(nobs if norm is not None else obs, nrew if norm is not None else rew, done)
+    r1.record(stream)
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ev = [x for x in ev if x is not None]
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    kts = np.array([s.elapsed_time(e) for s, e in ev]) if ev else None
+    if alone and TE == 0:
+        kern_ms = r0.elapsed_time(r1) / K
+        timing = f"one HIP event pair on the kernel's stream around all {K} timed launches (stream-busy time / {K})"
+    elif alone and TE > 1:
+        kern_ms = r0.elapsed_time(r1) / K
+        timing = (f"one HIP event pair on the kernel's stream around all {K} timed launches (stream-busy time / {K}, "
+                  f"including the markers around every {TE}th launch)")
+    else:
+        kern_ms = float(np.mean(kts))
+        timing = f"HIP events around each of the {K} timed k_step launches"
+    # the run must not hide a broken lane: loop-guard faults and non-finite outputs are checked
+    # over the timed window (status bit MRP_STATUS_NONFINITE marks a lane-step with NaN/inf)
+    flt = b.faults()
+    bad = {"lanes_with_loop_guard_fault": int(np.count_nonzero(flt)),
+           "obs_finite": bool(torch.isfinite(obs).all().item()),
+           "nonfinite_lane_steps": int(b.counters_ex()["nonfinite_steps"])}
     if distributed:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms, bad["lanes_with_loop_guard_fault"], 0 if bad["obs_finite"] else 1,
+                          bad["nonfinite_lane_steps"]], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
+        bad = {"lanes_with_loop_guard_fault": int(t[2]), "obs_finite": not bool(t[3]), "nonfinite_lane_steps": int(t[4])}
+    checks_ok = bad["lanes_with_loop_guard_fault"] == 0 and bad["obs_finite"] and bad["nonfinite_lane_steps"] == 0
 
-    toi, pos = b.counters() if rank == 0 else (0, 0)
-    # Diagnostics only (never `value`): per-launch spread of the timed window, and the rate over a
-    # later window of the same episodes (every lane spawned at step 0; the first tens of steps
-    # after a spawn carry most of the overlap resolution, so a window's rate depends on where it sits).
-    kts = np.array([s.elapsed_time(e) for s, e in ev])
+    ctr = b.counters_ex() if rank == 0 else {}
+    # Diagnostics only (never `value`): the rate over a later window of the same episodes (every
+    # lane spawned at step 0; the first tens of steps after a spawn carry most of the overlap
+    # resolution, so a window's rate depends on where it sits).
     later = None
     if args.later_window > 0 and rank == 0 and not distributed:
         skip = max(0, args.later_start - (args.warmup + K))
@@ -213,6 +311,43 @@ def main():
         e1.record(stream)
         torch.cuda.synchronize(dev)
         episode = {"steps": T, "env_steps_per_s": L * T / (e0.elapsed_time(e1) * 1e-3)}
+    # Diagnostic (never `value`): K env steps per launch (mrp_step_n_device) against single-step
+    # launches over the same window of the same trajectories (two batches, same seed): every step's
+    # outputs are written either way, so the gap is what the per-step max-over-lanes tail costs.
+    multi = None
+    if args.multi_step > 1 and rank == 0 and not distributed and norm is None:
+        Km, Tm = args.multi_step, args.multi_window
+        Tm = max(Km, Tm // Km * Km)
+        rates = {}
+        for mode in ("single", "multi"):
+            bm = Batch(args.env, L, device=local_rank, seed=args.seed + 1)
+            bm.set_stream(stream.cuda_stream)
+            bm.set_auto_reset(True)
+            bm.reset()
+            mo = torch.zeros((Km, L, O), dtype=torch.float32, device=dev)
+            mr = torch.zeros((Km, L), dtype=torch.float32, device=dev)
+            md = torch.zeros((Km, L), dtype=torch.uint8, device=dev)
+            for _ in range(args.warmup):
+                bm.step_device(0, mo.data_ptr(), mr.data_ptr(), md.data_ptr())
+            m0, m1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize(dev)
+            m0.record(stream)
+            if mode == "single":
+                for k in range(Tm):
+                    bm.step_device(0, mo[k % Km].data_ptr(), mr[k % Km].data_ptr(), md[k % Km].data_ptr())
+            else:
+                for _ in range(Tm // Km):
+                    bm.step_n_device(Km, 0, mo.data_ptr(), mr.data_ptr(), md.data_ptr())
+            m1.record(stream)
+            torch.cuda.synchronize(dev)
+            rates[mode] = L * Tm / (m0.elapsed_time(m1) * 1e-3)
+            bm.close()
+        multi = {"steps_per_launch": Km, "steps_after_spawn": [args.warmup + 1, args.warmup + Tm],
+                 "env_steps_per_s": rates["multi"], "single_step_launches_env_steps_per_s": rates["single"],
+                 "ratio": rates["multi"] / rates["single"]}
+    single = None
+    if args.single_env > 0 and rank == 0 and not distributed:
+        single = single_env_rate(ENV_NAMES[args.env] if args.env < 4 else "MultiRobotPuzzle-v0", args.single_env)
     if rank == 0:
         total_steps = world * L * K
         value = total_steps / elapsed
@@ -240,15 +375,18 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
                          "kernel": "k_step", "kernel_ms": kern_ms,
-                         "kernel_ms_timing": f"HIP events around every {TE}th timed launch ({len(ev)} launches)",
+                         "kernel_ms_timing": timing,
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "limiter": "latency: the serial Gauss-Seidel chains (velocity sweeps, position passes, TOI) of "
                                     "the slowest lanes, one wave's VALU issue; not HBM and not MFMA",
                          "note": "HBM fraction reported because the north star asks for it (SURVEY.md 8d)"},
-            "diagnostics": {"toi_events_total": toi, "position_iterations_total": pos,
+            "checks": dict(bad, ok=checks_ok),
+            "diagnostics": {"counters": ctr,
                             "timed_steps_after_spawn": [args.warmup + 1, args.warmup + K],
-                            "kernel_ms_min_median_max": [float(kts.min()), float(np.median(kts)), float(kts.max())],
-                            "later_window": later, "whole_episode": episode},
+                            "kernel_ms_min_median_max": None if kts is None else
+                            [float(kts.min()), float(np.median(kts)), float(kts.max())],
+                            "later_window": later, "whole_episode": episode, "multi_step_launch": multi,
+                            "single_env_drop_in": single},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.env, L, args.seed)
@@ -256,6 +394,9 @@ def main():
     b.close()
     if distributed:
         dist.destroy_process_group()
+    if not checks_ok:
+        print(f"bench.py: lane checks failed over the timed window: {bad}", file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

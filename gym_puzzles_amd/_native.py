@@ -16,6 +16,9 @@ LIB_PATH = os.path.join(_HERE, "libmrp.so")
 
 MRP_OK = 0
 STATUS_RUNNING, STATUS_PUZZLE_COMPLETE, STATUS_AGENT_OOB, STATUS_BLOCK_OOB = 0, 1, 2, 3
+STATUS_KIND_MASK, STATUS_NONFINITE, STATUS_FAULT = 0x3F, 0x40, 0x80   # include/mrp.h flag bits
+COUNTER_NAMES = ("steps", "resets", "toi_events", "position_iterations", "touching_contacts", "nonfinite_steps",
+                 "faulted_lanes")
 
 ENV_IDS = {
     "MultiRobotPuzzle-v0": 0,
@@ -32,11 +35,11 @@ EXPORTED = (
     "mrp_env_dims", "mrp_create", "mrp_destroy", "mrp_last_error", "mrp_n_lanes", "mrp_env_id",
     "mrp_set_stream", "mrp_synchronize", "mrp_set_reward_params", "mrp_update_params", "mrp_update_goal",
     "mrp_reset", "mrp_reset_device", "mrp_step", "mrp_step_device", "mrp_step_ex", "mrp_step_device_ex",
-    "mrp_set_auto_reset", "mrp_set_seed", "mrp_set_schedule",
-    "mrp_get_bodies", "mrp_get_flags", "mrp_get_faults", "mrp_counters", "mrp_state_words", "mrp_get_state", "mrp_set_state",
+    "mrp_step_n_device", "mrp_set_auto_reset", "mrp_set_seed", "mrp_set_schedule",
+    "mrp_get_bodies", "mrp_get_flags", "mrp_get_faults", "mrp_counters", "mrp_counters_ex", "mrp_state_words", "mrp_get_state", "mrp_set_state",
     "mrp_set_time_limit", "mrp_selftest_sincos", "mrp_debug_stamps", "mrp_debug_stamps_ext",
     "mrp_debug_trace", "mrp_debug_progress", "mrp_debug_velbench", "mrp_norm_create", "mrp_norm_destroy", "mrp_norm_last_error", "mrp_norm_set_stream",
-    "mrp_norm_set_training", "mrp_norm_reset_device", "mrp_norm_step_device", "mrp_norm_step_device_ex", "mrp_norm_get_stats", "mrp_norm_set_stats",
+    "mrp_norm_set_training", "mrp_norm_set_norm_obs", "mrp_norm_reset_device", "mrp_norm_step_device", "mrp_norm_step_device_ex", "mrp_norm_get_stats", "mrp_norm_set_stats",
     "mrp_render", "mrp_render_device", "mrp_get_goals", "mrp_shapes",
 )
 
@@ -77,6 +80,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.mrp_step_device.argtypes = [P, P, P, P, P, P, P, P]
     L.mrp_step_ex.argtypes = [P, P, P, P, P, P, P, P, P]
     L.mrp_step_device_ex.argtypes = [P, P, P, P, P, P, P, P, P]
+    L.mrp_step_n_device.argtypes = [P, i, P, P, P, P, P, P, P, P]
     L.mrp_set_seed.argtypes = [P, u64]
     L.mrp_set_schedule.argtypes = [P, i]
     L.mrp_set_auto_reset.argtypes = [P, i]
@@ -84,6 +88,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.mrp_get_flags.argtypes = [P, P]
     L.mrp_get_faults.argtypes = [P, P]
     L.mrp_counters.argtypes = [P, P, P]
+    L.mrp_counters_ex.argtypes = [P, P]
     L.mrp_state_words.argtypes = [i]
     L.mrp_get_state.argtypes = [P, P]
     L.mrp_set_state.argtypes = [P, P]
@@ -101,6 +106,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.mrp_norm_last_error.restype = ctypes.c_char_p
     L.mrp_norm_set_stream.argtypes = [P, P]
     L.mrp_norm_set_training.argtypes = [P, i]
+    L.mrp_norm_set_norm_obs.argtypes = [P, i]
     L.mrp_norm_reset_device.argtypes = [P, P, P]
     L.mrp_norm_step_device.argtypes = [P] * 10
     L.mrp_norm_step_device_ex.argtypes = [P] * 11
@@ -220,6 +226,13 @@ class Batch:
         self._check(load().mrp_step_device_ex(self._h, d_actions, d_obs, d_reward, d_reward64, d_done, d_trunc, d_status,
                                               d_term))
 
+    def step_n_device(self, n_steps, d_actions, d_obs, d_reward=None, d_done=None, d_trunc=None, d_status=None,
+                      d_term=None, d_reward64=None):
+        """``n_steps`` consecutive steps in one launch (mrp_step_n_device); every array holds
+        ``n_steps`` rows of ``n_lanes`` (step-major), device pointers as in step_device."""
+        self._check(load().mrp_step_n_device(self._h, int(n_steps), d_actions, d_obs, d_reward, d_reward64, d_done,
+                                             d_trunc, d_status, d_term))
+
     def set_schedule(self, mode):
         """Lane scheduling (mrp_set_schedule): 0 off, 1 costliest-first dispatch, 2 issue priority
         from the previous step's cost, 3 both (True = 1); results are identical in every mode."""
@@ -260,6 +273,12 @@ class Batch:
         b = np.zeros(1, np.int64)
         self._check(load().mrp_counters(self._h, _p(a), _p(b)))
         return int(a[0]), int(b[0])
+
+    def counters_ex(self) -> dict:
+        """Per-batch counters since creation (mrp_counters_ex; SURVEY.md 5 metrics)."""
+        out = np.zeros(8, np.int64)
+        self._check(load().mrp_counters_ex(self._h, _p(out)))
+        return {k: int(v) for k, v in zip(COUNTER_NAMES, out)}
 
     def get_state(self) -> np.ndarray:
         w = load().mrp_state_words(self.env_id)

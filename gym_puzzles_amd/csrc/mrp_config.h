@@ -10,6 +10,9 @@
 
 namespace mrp {
 
+// status byte flags next to the terminal kind (include/mrp.h MRP_STATUS_NONFINITE / MRP_STATUS_FAULT)
+constexpr int MRP_STATUS_NONFINITE_BIT = 0x40, MRP_STATUS_FAULT_BIT = 0x80;
+
 constexpr int MAX_POLY = 8;
 constexpr int TREE_N = 32;    // largest dynamic-tree node pool (15 proxies in the 3-block config)
 constexpr int MOVE_N = 16;    // move buffer: at most NF (<= 15) proxies move between two UpdatePairs

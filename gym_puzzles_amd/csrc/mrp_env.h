@@ -40,7 +40,7 @@ template <int ENV> struct Env : World<ENV> {
         for (int c = 0; c < D::CMAX; ++c) S.cnext[c] = c + 1 < D::CMAX ? c + 1 : NULLN;
         S.inv_dt0 = 0.0f; S.newFixture = 0; S.haveBodies = 0; S.episode = 0; S.stepCounter = 0;
         S.elapsed = 0; S.blks_in_place = 0; S.prev_blks_in_place = 0; S.wall_contact = 0;
-        S.toiEvents = 0; S.posIters = 0;
+        S.toiEvents = 0; S.posIters = 0; S.touching = 0; S.nonfinite = 0;
     }
 
     // _destroy (multi_robot_puzzle_00.py:218-229): blocks, walls, agents; each body's proxies

@@ -104,6 +104,7 @@ struct mrp_ctx {
     float* d_term = nullptr;
     float* d_bodies = nullptr;
     int32_t* d_flags = nullptr;
+    int64_t* d_ctr = nullptr;    // [CTR_N] mrp_counters_ex
     std::string err;
 };
 
@@ -146,7 +147,7 @@ void mrp_destroy(mrp_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     void* bufs[] = {ctx->d_state, ctx->d_draws, ctx->d_actions, ctx->d_mask, ctx->d_obs, ctx->d_reward, ctx->d_reward64,
-                    ctx->d_done, ctx->d_trunc, ctx->d_status, ctx->d_term, ctx->d_bodies, ctx->d_flags};
+                    ctx->d_done, ctx->d_trunc, ctx->d_status, ctx->d_term, ctx->d_bodies, ctx->d_flags, ctx->d_ctr};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (ctx->d_order) (void)hipFree(ctx->d_order);
@@ -205,6 +206,7 @@ int mrp_create(int env_id, int n_lanes, int device, uint64_t seed, uint64_t lane
         {(void**)&ctx->d_status, nl},
         {(void**)&ctx->d_bodies, nl * 6 * (ctx->n_agents + ctx->n_blocks) * sizeof(float)},
         {(void**)&ctx->d_flags, nl * (ctx->n_agents + 1) * sizeof(int32_t)},
+        {(void**)&ctx->d_ctr, CTR_N * sizeof(int64_t)},
     };
     for (auto& a : allocs)
         if ((e = hipMalloc(a.p, a.bytes)) != hipSuccess) return fail("hipMalloc", e);
@@ -308,15 +310,19 @@ int mrp_reset(mrp_ctx* ctx, const uint8_t* mask, const double* draws, const floa
     return MRP_OK;
 }
 
-int mrp_step_device_ex(mrp_ctx* ctx, const float* d_actions, float* d_obs, float* d_reward, double* d_reward64,
+static_assert(MRP_STATUS_NONFINITE == MRP_STATUS_NONFINITE_BIT && MRP_STATUS_FAULT == MRP_STATUS_FAULT_BIT,
+              "status flag bits of include/mrp.h and the kernels agree");
+
+static int step_launch(mrp_ctx* ctx, int n_steps, const float* d_actions, float* d_obs, float* d_reward, double* d_reward64,
                        uint8_t* d_done, uint8_t* d_trunc, uint8_t* d_status, float* d_term) {
-    if (!ctx || !d_obs) return MRP_E_ARG;
+    if (!ctx || !d_obs || n_steps < 1) return MRP_E_ARG;
     if (!ctx->have_reset) { ctx->err = "step() called before reset()"; return MRP_E_STATE; }
     HIPCHK(ctx, hipSetDevice(ctx->device));
     const int sched = ctx->schedule;
     StepArgs a{ctx->d_state, ctx->n_lanes, d_actions, d_obs, d_reward, d_reward64, d_done, d_trunc, d_status, d_term,
                ctx->params, ctx->seed, ctx->lane_offset, ctx->auto_reset, ctx->time_limit,
-               (sched & 1) ? ctx->d_order : nullptr, sched ? ctx->d_cost : nullptr, (sched & 2) ? ctx->d_costmax : nullptr};
+               (sched & 1) ? ctx->d_order : nullptr, sched ? ctx->d_cost : nullptr, (sched & 2) ? ctx->d_costmax : nullptr,
+               n_steps};
     env_ops(ctx->env_id)->step(ctx->stream, a);
     HIPCHK(ctx, hipGetLastError());
     if (sched) {   // next step's dispatch order / cost scale (stream-ordered behind this step)
@@ -325,6 +331,17 @@ int mrp_step_device_ex(mrp_ctx* ctx, const float* d_actions, float* d_obs, float
         HIPCHK(ctx, hipGetLastError());
     }
     return MRP_OK;
+}
+
+int mrp_step_device_ex(mrp_ctx* ctx, const float* d_actions, float* d_obs, float* d_reward, double* d_reward64,
+                       uint8_t* d_done, uint8_t* d_trunc, uint8_t* d_status, float* d_term) {
+    return step_launch(ctx, 1, d_actions, d_obs, d_reward, d_reward64, d_done, d_trunc, d_status, d_term);
+}
+
+int mrp_step_n_device(mrp_ctx* ctx, int n_steps, const float* d_actions, float* d_obs, float* d_reward, double* d_reward64,
+                      uint8_t* d_done, uint8_t* d_trunc, uint8_t* d_status, float* d_term) {
+    if (ctx && n_steps < 1) { ctx->err = "mrp_step_n_device: n_steps must be >= 1"; return MRP_E_ARG; }
+    return step_launch(ctx, n_steps, d_actions, d_obs, d_reward, d_reward64, d_done, d_trunc, d_status, d_term);
 }
 
 int mrp_step_device(mrp_ctx* ctx, const float* d_actions, float* d_obs, float* d_reward, uint8_t* d_done, uint8_t* d_trunc,
@@ -442,6 +459,16 @@ int mrp_counters(mrp_ctx* ctx, int64_t* toi_events, int64_t* pos_iters) {
     }
     if (toi_events) *toi_events = toi;
     if (pos_iters) *pos_iters = pos;
+    return MRP_OK;
+}
+
+int mrp_counters_ex(mrp_ctx* ctx, int64_t* out8) {
+    if (!ctx || !out8) return MRP_E_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    env_ops(ctx->env_id)->counters(ctx->stream, ctx->d_state, ctx->n_lanes, ctx->d_ctr);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemcpyAsync(out8, ctx->d_ctr, CTR_N * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     return MRP_OK;
 }
 

@@ -128,7 +128,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_reset(uint32_t* state, int nl, con
     store_state<ENV>(sh.S, state, lane, tid);
 }
 
-template <int ENV>
+template <int ENV, bool MULTI>
 #ifndef MRP_STEP_WAVES_PER_EU
 #define MRP_STEP_WAVES_PER_EU 4   // 4 waves per SIMD: all 4096 lanes of a GPU resident at once (LDS allows 16 per CU)
 #endif
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t*
                                                 double* reward64, uint8_t* done_out, uint8_t* trunc_out, uint8_t* status_out, float* term_obs,
                                                 EnvParams P, uint64_t seed, uint64_t lane_offset, int auto_reset,
                                                 int max_steps, const int* __restrict__ order, uint32_t* __restrict__ cost,
-                                                const uint32_t* __restrict__ costmax) {
+                                                const uint32_t* __restrict__ costmax, int nsteps) {
     using D = Dims<ENV>;
     __shared__ Shared<ENV> sh;
     __shared__ int s_fin;
@@ -160,40 +160,61 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t*
     toi0 = sh.S.toiEvents; pos0 = sh.S.posIters;
 #endif
     MRP_STAMP(0);
-    const uint64_t ctr = (uint64_t)sh.S.stepCounter * 64u;
-    if (tid < D::ACT)
-        sh.act[tid] = actions ? actions[(size_t)lane * D::ACT + tid] : (float)(-1.0 + 2.0 * rng_u01(seed, glane, 3, ctr + tid));
-    __syncthreads();
-    if (tid == 0) sh.S.stepCounter += 1;
     Env<ENV> e(sh, g_tables[ENV], P, tid);
     if (costmax) {   // priority from the lane's previous-step cost relative to the slowest lane's
         const uint64_t c = cost[lane], m = *costmax;
         e.prio_floor = __builtin_amdgcn_readfirstlane(4 * c > 3 * m ? 3 : (2 * c > m ? 2 : (4 * c > m ? 1 : 0)));
         e.set_prio(e.prio_floor);
     }
-    e.env_step_coop();
-    if (tid == 0) {
-        sh.S.elapsed += 1;
-        int d = sh.done, tr = 0;
-        if (max_steps > 0 && sh.S.elapsed >= max_steps) { tr = !d; d = 1; }   // gym TimeLimit
-        if (reward) reward[lane] = (float)sh.reward;
-        if (reward64) reward64[lane] = sh.reward;   // the reference's Python float
-        if (done_out) done_out[lane] = (uint8_t)d;
-        if (trunc_out) trunc_out[lane] = (uint8_t)tr;
-        if (status_out) status_out[lane] = (uint8_t)sh.kind;
-        s_fin = d;
+    // nsteps > 1 (mrp_step_n_device): the lane advances nsteps env steps with its state resident in
+    // LDS, writing every step's outputs (row s * nl + lane); each step is exactly one mrp_step
+    // (the single-step instantiation has a compile-time trip count of one, so none of the loop's
+    // state stays live across steps: the multi-step form carries more registers)
+    const int ns = MULTI ? nsteps : 1;
+    for (int s = 0; s < ns; ++s) {
+        const size_t row = (size_t)s * nl + lane;
+        const uint64_t ctr = (uint64_t)sh.S.stepCounter * 64u;
+        if (tid < D::ACT)
+            sh.act[tid] = actions ? actions[row * D::ACT + tid] : (float)(-1.0 + 2.0 * rng_u01(seed, glane, 3, ctr + tid));
+        __syncthreads();
+        if (tid == 0) sh.S.stepCounter += 1;
+        e.env_step_coop();
+        // per-lane failure report (SURVEY.md 8b Errors): a NaN / inf in the observation or the
+        // dynamic bodies' state, and a sticky loop-guard fault, set status bits (never a crash)
+        bool nf = false;
+        for (int k = tid; k < D::OBS; k += BLOCK) nf |= !__builtin_isfinite(sh.obs[k]);
+        if (tid < LaneState<ENV>::ND) {
+            const int b = tid;
+            nf |= !__builtin_isfinite(sh.S.cx[b]) || !__builtin_isfinite(sh.S.cy[b]) || !__builtin_isfinite(sh.S.a[b]) ||
+                  !__builtin_isfinite(sh.S.vx[b]) || !__builtin_isfinite(sh.S.vy[b]) || !__builtin_isfinite(sh.S.w[b]);
+        }
+        const bool nonfinite = __builtin_amdgcn_ballot_w64(nf) != 0;
+        if (tid == 0) {
+            sh.S.elapsed += 1;
+            int d = sh.done, tr = 0;
+            if (max_steps > 0 && sh.S.elapsed >= max_steps) { tr = !d; d = 1; }   // gym TimeLimit
+            if (nonfinite) sh.S.nonfinite += 1;
+            if (reward) reward[row] = (float)sh.reward;
+            if (reward64) reward64[row] = sh.reward;   // the reference's Python float
+            if (done_out) done_out[row] = (uint8_t)d;
+            if (trunc_out) trunc_out[row] = (uint8_t)tr;
+            if (status_out)
+                status_out[row] = (uint8_t)(sh.kind | (nonfinite ? MRP_STATUS_NONFINITE_BIT : 0) |
+                                            (sh.S.fault ? MRP_STATUS_FAULT_BIT : 0));
+            s_fin = d;
+        }
+        __syncthreads();
+        if (term_obs)
+            for (int k = tid; k < D::OBS; k += BLOCK) term_obs[row * D::OBS + k] = sh.obs[k];
+        MRP_STAMP(8);
+        if (s_fin && auto_reset) {   // SB3-style auto-reset with device-RNG spawns
+            stage_reset_inputs<ENV>(sh, nullptr, nullptr, lane, tid, seed, glane);
+            e.env_reset_coop();
+            MRP_STAMP(9);
+        }
+        for (int k = tid; k < D::OBS; k += BLOCK) obs[row * D::OBS + k] = sh.obs[k];
+        __syncthreads();
     }
-    __syncthreads();
-    float* orow = obs + (size_t)lane * D::OBS;
-    if (term_obs)
-        for (int k = tid; k < D::OBS; k += BLOCK) term_obs[(size_t)lane * D::OBS + k] = sh.obs[k];
-    MRP_STAMP(8);
-    if (s_fin && auto_reset) {   // SB3-style auto-reset with device-RNG spawns
-        stage_reset_inputs<ENV>(sh, nullptr, nullptr, lane, tid, seed, glane);
-        e.env_reset_coop();
-        MRP_STAMP(9);
-    }
-    for (int k = tid; k < D::OBS; k += BLOCK) orow[k] = sh.obs[k];
     store_state<ENV>(sh.S, state, lane, tid);
     if (cost && tid == 0) cost[lane] = (uint32_t)min(__builtin_amdgcn_s_memtime() - t_start, 0xffffffffull);
     MRP_STAMP(10);
@@ -242,6 +263,28 @@ __global__ __launch_bounds__(256) void k_faults(const uint32_t* state, int nl, i
     out[lane] = S.fault;
 }
 
+// per-lane counters summed over the lanes (one workgroup; a tree reduction in LDS, no atomics)
+template <int ENV>
+__global__ __launch_bounds__(256) void k_counters(const uint32_t* state, int nl, int64_t* out) {
+    __shared__ long long red[CTR_N][256];
+    const int t = threadIdx.x;
+    long long acc[CTR_N] = {};
+    for (int lane = t; lane < nl; lane += 256) {
+        const LaneState<ENV>& S = *reinterpret_cast<const LaneState<ENV>*>(state + (size_t)lane * lane_words<ENV>());
+        acc[CTR_STEPS] += S.stepCounter; acc[CTR_RESETS] += S.episode; acc[CTR_TOI] += S.toiEvents;
+        acc[CTR_POS_ITERS] += S.posIters; acc[CTR_TOUCHING] += S.touching; acc[CTR_NONFINITE] += S.nonfinite;
+        acc[CTR_FAULT_LANES] += S.fault != 0;
+    }
+    for (int k = 0; k < CTR_N; ++k) red[k][t] = acc[k];
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (t < w)
+            for (int k = 0; k < CTR_N; ++k) red[k][t] += red[k][t + w];
+        __syncthreads();
+    }
+    if (t < CTR_N) out[t] = red[t][0];
+}
+
 // ------------------------------------------------------------------------------ launch table
 template <int ENV>
 struct Launch {
@@ -256,15 +299,23 @@ struct Launch {
         hipLaunchKernelGGL(k_reset<ENV>, dim3(nl), dim3(BLOCK), 0, s, state, nl, mask, draws, actions, obs, P, seed, lane_offset);
     }
     static void step(hipStream_t s, const StepArgs& a) {
-        hipLaunchKernelGGL(k_step<ENV>, dim3(a.nl), dim3(BLOCK), 0, s, a.state, a.nl, a.actions, a.obs, a.reward, a.reward64,
-                           a.done, a.trunc, a.status, a.term_obs, a.P, a.seed, a.lane_offset, a.auto_reset, a.max_steps,
-                           a.order, a.cost, a.costmax);
+        if (a.nsteps > 1)
+            hipLaunchKernelGGL((k_step<ENV, true>), dim3(a.nl), dim3(BLOCK), 0, s, a.state, a.nl, a.actions, a.obs, a.reward,
+                               a.reward64, a.done, a.trunc, a.status, a.term_obs, a.P, a.seed, a.lane_offset, a.auto_reset,
+                               a.max_steps, a.order, a.cost, a.costmax, a.nsteps);
+        else
+            hipLaunchKernelGGL((k_step<ENV, false>), dim3(a.nl), dim3(BLOCK), 0, s, a.state, a.nl, a.actions, a.obs, a.reward,
+                               a.reward64, a.done, a.trunc, a.status, a.term_obs, a.P, a.seed, a.lane_offset, a.auto_reset,
+                               a.max_steps, a.order, a.cost, a.costmax, 1);
     }
     static void bodies(hipStream_t s, const uint32_t* state, int nl, float* out, int32_t* flags) {
         hipLaunchKernelGGL(k_bodies<ENV>, dim3(nl), dim3(BLOCK), 0, s, state, nl, out, flags);
     }
     static void faults(hipStream_t s, const uint32_t* state, int nl, int32_t* out) {
         hipLaunchKernelGGL(k_faults<ENV>, dim3((nl + 255) / 256), dim3(256), 0, s, state, nl, out);
+    }
+    static void counters(hipStream_t s, const uint32_t* state, int nl, int64_t* out) {
+        hipLaunchKernelGGL(k_counters<ENV>, dim3(1), dim3(256), 0, s, state, nl, out);
     }
     static void render(hipStream_t s, dim3 grid, const uint32_t* state, const int32_t* lanes, int nl, int W, int H,
                        const mrpr::RenderArgs& A, uint8_t* rgb) {
@@ -298,7 +349,7 @@ struct Launch {
     }
     static constexpr EnvOps ops() {
         return EnvOps{lane_words<ENV>(), (int)(offsetof(LaneState<ENV>, toiEvents) / 4), upload_tables, init, reset, step,
-                      bodies, faults, render, goals, debug_read, debug_progress};
+                      bodies, faults, counters, render, goals, debug_read, debug_progress};
     }
 };
 

@@ -146,7 +146,7 @@ thread_local std::string g_norm_create_error;
 }  // namespace
 
 struct mrp_norm {
-    int n_lanes = 0, obs_dim = 0, device = 0, training = 1;
+    int n_lanes = 0, obs_dim = 0, device = 0, training = 1, norm_obs = 1;
     double clip_obs = 10.0, clip_rew = 10.0, gamma = 0.99, eps = 1e-8;
     hipStream_t stream = nullptr, own_stream = nullptr;
     double* d_stats = nullptr;   // [obs_mean D][obs_var D][obs_count][ret mean, var, count]
@@ -241,11 +241,18 @@ int mrp_norm_set_training(mrp_norm* n, int training) {
     return MRP_OK;
 }
 
+int mrp_norm_set_norm_obs(mrp_norm* n, int norm_obs) {
+    if (!n) return MRP_E_ARG;
+    n->norm_obs = norm_obs ? 1 : 0;
+    return MRP_OK;
+}
+
 static int norm_launch(mrp_norm* n, const float* obs, const float* reward, const double* reward64, const uint8_t* done,
                        const float* term, float* obs_out, float* reward_out, float* term_out, double* ep_ret_out, int* ep_len_out, int step) {
     NCHK(n, hipSetDevice(n->device));
     const int L = n->n_lanes, D = n->obs_dim;
-    const int upd_obs = n->training, upd_ret = step && n->training;
+    // SB3 VecNormalize: obs statistics move when training and norm_obs, the returns' when training
+    const int upd_obs = n->training && n->norm_obs, upd_ret = step && n->training;
     if (upd_obs || upd_ret) {
         hipLaunchKernelGGL(k_moments, dim3(D + 1), dim3(NT), 0, n->stream, obs, L, D, reward, n->d_returns, n->gamma,
                            n->obs_mean(), n->obs_var(), n->obs_count(), n->ret_stats(), upd_obs, upd_ret);

@@ -46,7 +46,11 @@ struct StepArgs {
     const int* order;          // NULL: workgroup b steps lane b
     uint32_t* cost;            // NULL: no per-lane cycle record
     const uint32_t* costmax;   // NULL: no cost-derived priority
+    int nsteps;                // env steps per launch (mrp_step_n_device); step s of lane l writes row s * nl + l
 };
+
+// per-lane counters summed over the lanes (mrp_counters_ex), in this order
+enum : int { CTR_STEPS = 0, CTR_RESETS, CTR_TOI, CTR_POS_ITERS, CTR_TOUCHING, CTR_NONFINITE, CTR_FAULT_LANES, CTR_N = 8 };
 
 // diagnostic symbols of a -DMRP_STAMPS / -DMRP_PROGRESS build (debug_read's `what`)
 enum : int { DBG_STAMPS = 0, DBG_PMAX = 1, DBG_STEPMAX = 2, DBG_RT = 3, DBG_TRACE = 4 };
@@ -61,6 +65,7 @@ struct EnvOps {
     void (*step)(hipStream_t, const StepArgs& a);
     void (*bodies)(hipStream_t, const uint32_t* state, int nl, float* out, int32_t* flags);
     void (*faults)(hipStream_t, const uint32_t* state, int nl, int32_t* out);
+    void (*counters)(hipStream_t, const uint32_t* state, int nl, int64_t* out /* [CTR_N] */);
     void (*render)(hipStream_t, dim3 grid, const uint32_t* state, const int32_t* lanes, int nl, int W, int H,
                    const mrpr::RenderArgs& A, uint8_t* rgb);
     void (*goals)(hipStream_t, const uint32_t* state, int nl, double* out);

@@ -74,6 +74,11 @@ static __device__ uint32_t* g_progress;
 // corrupted lane finishes its step (and is reported by mrp_get_faults) instead of hanging the GPU.
 constexpr int MRP_FAULT_TREE_UP = 1, MRP_FAULT_TREE_DOWN = 2, MRP_FAULT_TREE_REMOVE = 3, MRP_FAULT_CONTACT_LIST = 4,
               MRP_FAULT_ISLANDS = 5, MRP_FAULT_TOI_PASSES = 6, MRP_FAULT_PAIR_DECODE = 7, MRP_FAULT_DFS = 8;
+// Pool guards: the fixed per-lane pools (tree nodes, contact slots, move buffer, island arrays) are
+// sized from the configs' geometry and never fill in a valid world (tests/test_oracle.py checks the
+// oracle's high-water marks against them); a full pool records its code and the insertion is
+// skipped, so no index ever leaves its array.
+constexpr int MRP_FAULT_TREE_POOL = 9, MRP_FAULT_CONTACT_POOL = 10, MRP_FAULT_MOVE_BUFFER = 11, MRP_FAULT_ISLAND_POOL = 12;
 constexpr float LINEAR_SLOP = 0.005f;
 constexpr float AABB_EXT = 0.1f;
 constexpr float AABB_MUL = 2.0f;
@@ -133,6 +138,8 @@ template <int ENV> struct alignas(16) LaneState {   // 16-B granules: moved with
     double block_distance[D::NB];
     double goal[D::NB][3];
     long long toiEvents, posIters;
+    long long touching;    // touching contacts after each world.Step's Collide, summed (SURVEY.md 5 metrics)
+    long long nonfinite;   // steps whose observation or body state held a NaN / inf
 };
 
 template <int ENV> constexpr int lane_words() { return (int)(sizeof(LaneState<ENV>) / 4); }
@@ -276,6 +283,7 @@ template <int ENV> struct World {
     __device__ __forceinline__ static float perim(float lx, float ly, float hx, float hy) { float wx = hx - lx; float wy = hy - ly; return 2.0f * (wx + wy); }
     __device__ __forceinline__ int t_alloc() {
         int id = S.freeList;
+        if ((unsigned)id >= (unsigned)LS::TN) { S.fault = MRP_FAULT_TREE_POOL; id = LS::TN - 1; }   // never in a valid world
         S.freeList = S.tpar[id];
         S.tpar[id] = NULLN; S.tc1[id] = NULLN; S.tc2[id] = NULLN; S.th[id] = 0; S.tud[id] = -1;
         ++S.nodeCount;
@@ -402,7 +410,10 @@ template <int ENV> struct World {
             S.root = sibling; S.tpar[sibling] = NULLN; t_free(parent);
         }
     }
-    __device__ __forceinline__ void buffer_move(int id) { S.moveBuf[S.moveCount++] = id; }
+    __device__ __forceinline__ void buffer_move(int id) {
+        if (S.moveCount >= MOVE_N) { S.fault = MRP_FAULT_MOVE_BUFFER; return; }   // never in a valid world
+        S.moveBuf[S.moveCount++] = id;
+    }
     __device__ __forceinline__ void unbuffer_move(int id) { for (int i = 0; i < S.moveCount; ++i) if (S.moveBuf[i] == id) S.moveBuf[i] = NULLN; }
 
     // polygon AABB under a transform (b2PolygonShape::ComputeAABB)
@@ -480,6 +491,7 @@ template <int ENV> struct World {
         }
         if (!is_dyn(bA) && !is_dyn(bB)) return;
         int c = S.cFree;
+        if ((unsigned)c >= (unsigned)C) { S.fault = MRP_FAULT_CONTACT_POOL; return; }   // never in a valid world
         S.cFree = S.cnext[c];
         S.cfa[c] = fa; S.cfb[c] = fb; S.cflags[c] = CF_ENABLED; S.ctoiCount[c] = 0; S.ctoi[c] = 1.0f;
         S.cfric[c] = sqrtf(L.fix_friction[fa] * L.fix_friction[fb]);
@@ -700,6 +712,7 @@ template <int ENV> struct World {
             touching += __popcll(__ballot(t));
         }
         touching = __builtin_amdgcn_readfirstlane(touching);
+        if (tid == 0) S.touching += touching;
         step_prio = touching >= 4 ? 2 : (touching >= 2 ? 1 : 0);
         if (prio_floor > step_prio) step_prio = prio_floor;
         set_prio(step_prio);
@@ -1621,6 +1634,7 @@ template <int ENV> struct World {
                             if (bA != b && bB != b) continue;
                             if (S.cflags[c] & CF_ISLAND) continue;
                             if ((S.cflags[c] & CF_ENABLED) == 0 || (S.cflags[c] & CF_TOUCHING) == 0) continue;
+                            if (is.nc >= C || sc >= NBODY) { S.fault = MRP_FAULT_ISLAND_POOL; continue; }   // never in a valid world
                             is.contacts[is.nc++] = c;
                             S.cflags[c] |= CF_ISLAND;
                             int other = bA == b ? bB : bA;
@@ -2041,6 +2055,7 @@ template <int ENV> struct World {
                 if (cA != body && cB != body) continue;
                 if (is.nb == 2 * MAX_TOI_CONTACTS) break;
                 if (is.nc == MAX_TOI_CONTACTS) break;
+                if (is.nc >= C || is.nb >= NBODY) { S.fault = MRP_FAULT_ISLAND_POOL; break; }   // never in a valid world
                 if (S.cflags[c] & CF_ISLAND) continue;
                 int other = cA == body ? cB : cA;
                 if (is_dyn(other)) continue;   // only static bodies join a TOI island here

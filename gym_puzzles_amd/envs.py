@@ -27,7 +27,8 @@ from __future__ import annotations
 
 import numpy as np
 
-from ._native import STATUS_AGENT_OOB, STATUS_BLOCK_OOB, STATUS_PUZZLE_COMPLETE, Batch
+from ._native import (STATUS_AGENT_OOB, STATUS_BLOCK_OOB, STATUS_FAULT, STATUS_KIND_MASK, STATUS_NONFINITE,
+                      STATUS_PUZZLE_COMPLETE, Batch)
 from .seeding import make_box, np_random
 from .spawn import reference_draws
 
@@ -70,13 +71,21 @@ class _MRPBase:
     def step(self, action):
         a = np.asarray(action, dtype=np.float32).reshape(1, -1)
         obs, rew, done, _ = self._b.step(a)
-        st = int(self._b.status[0])
+        flags = int(self._b.status[0])
+        st = flags & STATUS_KIND_MASK
         self.done_status = _DONE_STATUS.get(st)
         if st != 0 and self._needs_shaped() and not self._params_updated:
             name = "shaped_bounds_penalty" if st == STATUS_AGENT_OOB else (
                 "shaped_blk_bounds_penalty" if st == STATUS_BLOCK_OOB else "shaped_puzzle_reward")
             raise AttributeError(f"'{type(self).__name__}' object has no attribute '{name}'")
-        return obs[0].astype(np.float64), float(self._b.reward64[0]), bool(done[0]), {}
+        # the reference returns {} (multi_robot_puzzle_00.py:521); a broken lane is reported, never
+        # raised (SURVEY.md 8b Errors): info['nan'] on a NaN/inf step, info['mrp_fault'] = guard code
+        info = {}
+        if flags & STATUS_NONFINITE:
+            info["nan"] = True
+        if flags & STATUS_FAULT:
+            info["mrp_fault"] = int(self._b.faults()[0])
+        return obs[0].astype(np.float64), float(self._b.reward64[0]), bool(done[0]), info
 
     def render(self, mode="human", close=False):
         if close:
@@ -312,13 +321,21 @@ def make(env_id: str, **kwargs):
     return TimeLimit(cls(**kwargs), max_steps)
 
 
-def register_with_gym() -> bool:
-    """Register the ids with gym's registry when gym is importable (it is not in this image)."""
+def register_with_gym(alias_suffix: str = "-mi355x") -> dict:
+    """Register the reference's ids (gym_puzzles/__init__.py:3-35) with gym's registry when gym is
+    importable (it is not in this image), so ``gym.make('MultiRobotPuzzle-v0')`` builds this
+    package's class, as the drop-in contract asks.  An id the registry already holds (the
+    reference package imported first) is left alone and registered under ``id + alias_suffix``.
+    Returns {reference id: registered id}; empty without gym."""
     try:
-        from gym.envs.registration import register
+        from gym.envs.registration import register, registry
     except ImportError:
-        return False
+        return {}
+    have = set(getattr(registry, "env_specs", registry).keys()) if hasattr(registry, "keys") or hasattr(registry, "env_specs") else set()
+    out = {}
     for name, (cls, max_steps) in ENV_CLASSES.items():
-        register(id=name + "-mi355x", entry_point=f"gym_puzzles_amd.envs:{cls.__name__}",
+        rid = name if name not in have else name + alias_suffix
+        register(id=rid, entry_point=f"gym_puzzles_amd.envs:{cls.__name__}",
                  max_episode_steps=max_steps, reward_threshold=REWARD_THRESHOLD.get(name, 500))
-    return True
+        out[name] = rid
+    return out

@@ -118,7 +118,19 @@ class Box:
 def make_box(low, high, shape=None, dtype=np.float32):
     """The env's observation/action space: ``gym.spaces.Box`` when gym is importable (SB3's
     wrappers and policies dispatch on ``isinstance(space, gym.spaces.Box)``), else the numpy
-    restatement above (same bounds, dtype and sampling algorithm)."""
+    restatement above (same bounds, dtype and sampling algorithm).  stable-baselines3 2.x checks
+    for gymnasium spaces, so with SB3 >= 2 installed the space is ``gymnasium.spaces.Box``."""
+    try:
+        import stable_baselines3
+        sb3_major = int(stable_baselines3.__version__.split(".")[0])
+    except (ImportError, ValueError, AttributeError):
+        sb3_major = 0
+    if sb3_major >= 2:
+        try:
+            from gymnasium import spaces
+            return spaces.Box(low, high, shape=shape, dtype=dtype)
+        except ImportError:
+            pass
     try:
         from gym import spaces
     except ImportError:

@@ -21,7 +21,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from ._native import ENV_IDS, Batch, env_dims
+from ._native import ENV_IDS, STATUS_FAULT, STATUS_NONFINITE, Batch, env_dims
 from .seeding import make_box
 
 try:   # SB3 1.x/2.x: VecEnv(num_envs, observation_space, action_space)
@@ -30,6 +30,20 @@ except ImportError:
     _VecEnvBase = object
 
 _ID = dict(ENV_IDS)
+
+
+def _lane_flags(batch: Batch, status: np.ndarray, infos: list) -> None:
+    """Per-lane failure report (SURVEY.md 8b Errors): ``info['nan']`` for a lane whose step
+    produced a NaN / inf, ``info['mrp_fault']`` = the loop-guard code of a lane whose guard has
+    tripped (include/mrp.h status flag bits).  Never raises; healthy lanes get no extra keys."""
+    nan = np.nonzero(status & STATUS_NONFINITE)[0]
+    for i in nan:
+        infos[i]["nan"] = True
+    bad = np.nonzero(status & STATUS_FAULT)[0]
+    if bad.size:
+        codes = batch.faults()
+        for i in bad:
+            infos[i]["mrp_fault"] = int(codes[i])
 
 
 class MultiRobotPuzzleVecEnv(_VecEnvBase):
@@ -43,13 +57,15 @@ class MultiRobotPuzzleVecEnv(_VecEnvBase):
         self._lane_offset = lane_offset
         self.observation_space = make_box(-np.inf, np.inf, shape=(d["obs_dim"],), dtype=np.float32)
         self.action_space = make_box(-1.0, 1.0, shape=(d["act_dim"],), dtype=np.float32)
-        if _VecEnvBase is not object:
-            _VecEnvBase.__init__(self, num_envs, self.observation_space, self.action_space)
         self.max_episode_steps = d["max_episode_steps"] if max_episode_steps is None else max_episode_steps
+        # everything get_attr / step need exists before SB3's base __init__ runs (SB3 2.x queries
+        # get_attr("render_mode") from it)
+        self._attrs = {"render_mode": None}
+        self._actions = None
         self._b = None
         self._make_batch()
-        self._actions = None
-        self._attrs = {}
+        if _VecEnvBase is not object:
+            _VecEnvBase.__init__(self, num_envs, self.observation_space, self.action_space)
 
     def _make_batch(self):
         if self._b is not None:
@@ -72,6 +88,7 @@ class MultiRobotPuzzleVecEnv(_VecEnvBase):
         for i in np.nonzero(done)[0]:
             infos[i]["terminal_observation"] = self._b.terminal_obs[i].copy()
             infos[i]["TimeLimit.truncated"] = bool(trunc[i])
+        _lane_flags(self._b, self._b.status, infos)
         return obs.copy(), rew.copy(), done.astype(bool), infos
 
     def step(self, actions):
@@ -123,19 +140,19 @@ class MultiRobotPuzzleVecEnv(_VecEnvBase):
         return list(indices)
 
     # -- zero-copy device path -----------------------------------------------------------------
-    def step_torch(self, actions, obs, reward, done, truncated=None, terminal_obs=None, reward64=None):
+    def step_torch(self, actions, obs, reward, done, truncated=None, terminal_obs=None, reward64=None, status=None):
         """One step on torch CUDA tensors on this env's device (float32 [N, A] actions, [N, O] obs,
-        [N] reward, uint8 [N] done/truncated, optional [N, O] terminal_obs and float64 [N]
+        [N] reward, uint8 [N] done/truncated/status, optional [N, O] terminal_obs and float64 [N]
         reward64), asynchronous on that device's current torch stream."""
         import torch
         dev = torch.device("cuda", self.device)
         for name, t in (("actions", actions), ("obs", obs), ("reward", reward), ("done", done), ("truncated", truncated),
-                        ("terminal_obs", terminal_obs), ("reward64", reward64)):
+                        ("terminal_obs", terminal_obs), ("reward64", reward64), ("status", status)):
             if t is not None and t.device != dev:
                 raise ValueError(f"step_torch: {name} is on {t.device}, this VecEnv runs on {dev}")
         self._b.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         ptr = (lambda t: 0 if t is None else t.data_ptr())
-        self._b.step_device(ptr(actions), obs.data_ptr(), reward.data_ptr(), done.data_ptr(), ptr(truncated), 0,
+        self._b.step_device(ptr(actions), obs.data_ptr(), reward.data_ptr(), done.data_ptr(), ptr(truncated), ptr(status),
                             ptr(terminal_obs), ptr(reward64))
 
     @property
@@ -162,6 +179,7 @@ class DeviceVecNormalize:
             raise MrpError(f"mrp_norm_create failed ({rc}): {self._L.mrp_norm_last_error(None).decode()}")
         self._h = h
         self._training = True
+        self._norm_obs = True
 
     def _check(self, rc):
         if rc != 0:
@@ -179,6 +197,16 @@ class DeviceVecNormalize:
     def training(self, value: bool):
         self._training = bool(value)
         self._check(self._L.mrp_norm_set_training(self._h, int(self._training)))
+
+    @property
+    def norm_obs(self) -> bool:
+        return self._norm_obs
+
+    @norm_obs.setter
+    def norm_obs(self, value: bool):
+        """SB3 VecNormalize.norm_obs: the observation statistics only move while it is set."""
+        self._norm_obs = bool(value)
+        self._check(self._L.mrp_norm_set_norm_obs(self._h, int(self._norm_obs)))
 
     def reset(self, obs, obs_out):
         self._sync_stream()
@@ -228,21 +256,23 @@ class MultiRobotPuzzleVecNormalize:
                  clip_obs: float = 10.0, clip_reward: float = 10.0, gamma: float = 0.99, epsilon: float = 1e-8):
         import torch
         self.venv = venv
-        # SB3 semantics: the flags choose what step()/reset() return; the running statistics are
-        # updated whenever `training` is set, whatever the flags
-        self.norm_obs, self.norm_reward = bool(norm_obs), bool(norm_reward)
+        # SB3 semantics: the flags choose what step()/reset() return; while `training` is set the
+        # returns' statistics are updated, and the observation statistics only when norm_obs is set
+        self.norm_reward = bool(norm_reward)
         self.clip_obs, self.clip_reward, self.gamma, self.epsilon = clip_obs, clip_reward, gamma, epsilon
         self.num_envs, self.observation_space, self.action_space = venv.num_envs, venv.observation_space, venv.action_space
         N, O = venv.num_envs, venv.observation_space.shape[0]
         dev = torch.device("cuda", venv.device)
         self.norm = DeviceVecNormalize(N, O, venv.device, clip_obs, clip_reward, gamma, epsilon)
         self.norm.training = training
+        self.norm.norm_obs = norm_obs
         z = lambda *s, dt=torch.float32: torch.zeros(s, dtype=dt, device=dev)  # noqa: E731
         self._act, self._obs, self._rew = z(N, venv.action_space.shape[0]), z(N, O), z(N)
         self._done, self._trunc, self._term = z(N, dt=torch.uint8), z(N, dt=torch.uint8), z(N, O)
         self._nobs, self._nrew, self._nterm = z(N, O), z(N), z(N, O)
         self._epr, self._epl = z(N, dt=torch.float64), z(N, dt=torch.int32)
         self._rew64 = z(N, dt=torch.float64)
+        self._status = z(N, dt=torch.uint8)
 
     @property
     def training(self):
@@ -251,6 +281,14 @@ class MultiRobotPuzzleVecNormalize:
     @training.setter
     def training(self, v):
         self.norm.training = v
+
+    @property
+    def norm_obs(self):
+        return self.norm.norm_obs
+
+    @norm_obs.setter
+    def norm_obs(self, v):
+        self.norm.norm_obs = v
 
     def reset(self):
         import torch
@@ -261,7 +299,7 @@ class MultiRobotPuzzleVecNormalize:
     def step(self, actions):
         import torch
         self._act.copy_(torch.as_tensor(np.asarray(actions, np.float32).reshape(self.num_envs, -1)))
-        self.venv.step_torch(self._act, self._obs, self._rew, self._done, self._trunc, self._term, self._rew64)
+        self.venv.step_torch(self._act, self._obs, self._rew, self._done, self._trunc, self._term, self._rew64, self._status)
         self.norm.step(self._obs, self._rew, self._done, self._nobs, self._nrew, self._term, self._nterm, self._epr, self._epl,
                        self._rew64)
         obs = (self._nobs if self.norm_obs else self._obs).cpu().numpy()
@@ -276,6 +314,7 @@ class MultiRobotPuzzleVecNormalize:
                 infos[i]["terminal_observation"] = term[i].copy()
                 infos[i]["TimeLimit.truncated"] = bool(trunc[i])
                 infos[i]["episode"] = {"r": round(float(epr[i]), 6), "l": int(epl[i])}
+        _lane_flags(self.venv.batch, self._status.cpu().numpy(), infos)
         return obs, rew, done, infos
 
     def get_original_obs(self):
@@ -285,9 +324,12 @@ class MultiRobotPuzzleVecNormalize:
     # SB3 pickles the wrapper; this build stores the same statistics and settings in an .npz
     # (nothing in the file is executed on load).
     def save(self, save_path: str) -> None:
+        """Writes exactly `save_path` (train.py:149 saves to 'models/<run>/saved_env.pkl' and
+        test.py:66 loads that same path back; np.savez on a bare path would append '.npz')."""
         st = self.norm.get_stats()
-        np.savez(save_path, **st, clip_obs=self.clip_obs, clip_reward=self.clip_reward, gamma=self.gamma,
-                 epsilon=self.epsilon, training=self.training, norm_obs=self.norm_obs, norm_reward=self.norm_reward)
+        with open(save_path, "wb") as f:
+            np.savez(f, **st, clip_obs=self.clip_obs, clip_reward=self.clip_reward, gamma=self.gamma,
+                     epsilon=self.epsilon, training=self.training, norm_obs=self.norm_obs, norm_reward=self.norm_reward)
 
     @classmethod
     def load(cls, load_path: str, venv: MultiRobotPuzzleVecEnv) -> "MultiRobotPuzzleVecNormalize":

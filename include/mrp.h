@@ -42,6 +42,11 @@ extern "C" {
 #define MRP_STATUS_PUZZLE_COMPLETE 1   /* multi_robot_puzzle_00.py:515-519, _02.py:575-582 */
 #define MRP_STATUS_AGENT_OOB 2         /* multi_robot_puzzle_02.py:552-556 */
 #define MRP_STATUS_BLOCK_OOB 3         /* multi_robot_puzzle_02.py:558-562 */
+/* flag bits OR-ed into the status byte (SURVEY.md 8b "Errors": per-lane NaN is reported, never a
+ * crash; the reference would carry the NaN on silently, multi_robot_puzzle_00.py:521 returns {}) */
+#define MRP_STATUS_KIND_MASK 0x3f
+#define MRP_STATUS_NONFINITE 0x40      /* this step's observation or a dynamic body's state holds NaN/inf */
+#define MRP_STATUS_FAULT 0x80          /* a loop guard has tripped in this lane (sticky; code: mrp_get_faults) */
 
 typedef struct mrp_ctx mrp_ctx;
 
@@ -110,6 +115,14 @@ int mrp_step_ex(mrp_ctx* ctx, const float* actions, float* obs, float* reward, d
                 uint8_t* truncated, uint8_t* status, float* terminal_obs);
 int mrp_step_device_ex(mrp_ctx* ctx, const float* d_actions, float* d_obs, float* d_reward, double* d_reward64,
                        uint8_t* d_done, uint8_t* d_truncated, uint8_t* d_status, float* d_terminal_obs);
+/* n_steps consecutive step() calls of every lane in ONE launch (synthetic rollouts, evaluation
+ * with device-RNG or pre-computed actions): the lane state stays on chip between the steps, and
+ * each step writes its outputs exactly as one mrp_step_device_ex would (step s of lane l at row
+ * s * n_lanes + l of every array: d_actions [n_steps][n_lanes][act_dim] or NULL = device RNG,
+ * d_obs / d_terminal_obs [n_steps][n_lanes][obs_dim], the others [n_steps][n_lanes]).  The result
+ * is bit-identical to n_steps single steps; lanes advance independently inside the launch. */
+int mrp_step_n_device(mrp_ctx* ctx, int n_steps, const float* d_actions, float* d_obs, float* d_reward, double* d_reward64,
+                      uint8_t* d_done, uint8_t* d_truncated, uint8_t* d_status, float* d_terminal_obs);
 int mrp_set_auto_reset(mrp_ctx* ctx, int enabled);
 /* Re-key the device counter RNG (spawns of later resets, synthetic actions) without touching the
  * lanes, parameters, stream or time limit: SB3 VecEnv.seed(seed) (train/train.py:63-75 seeds
@@ -130,10 +143,16 @@ int mrp_get_bodies(mrp_ctx* ctx, float* out /* [n_lanes][6*(n_blocks+n_agents)] 
 int mrp_get_flags(mrp_ctx* ctx, int32_t* out);
 /* per lane: 0, or the code of the loop guard that ended a runaway loop in that lane (a bound no
  * valid world reaches: tree walks, contact-list walks, islands, TOI passes; see mrp_world.h
- * MRP_FAULT_*).  Sticky.  int32 [n_lanes] */
+ * MRP_FAULT_*: 1-8 loop guards -- tree walks, contact-list walks, islands, TOI passes, pair decoding,
+ * island DFS; 9-12 pool guards -- tree nodes, contact slots, move buffer, island arrays).  Sticky.
+ * int32 [n_lanes] */
 int mrp_get_faults(mrp_ctx* ctx, int32_t* out);
 /* summed over lanes: TOI events and position-solver iterations (diagnostics) */
 int mrp_counters(mrp_ctx* ctx, int64_t* toi_events, int64_t* pos_iters);
+/* per-batch counters (SURVEY.md 5 "Metrics"), summed over lanes since mrp_create, reduced on the
+ * device: out[8] = steps, resets, TOI events, position iterations, touching contacts (after each
+ * world.Step's Collide), lane-steps with a non-finite output, lanes with a tripped loop guard, 0 */
+int mrp_counters_ex(mrp_ctx* ctx, int64_t* out8);
 /* Raw per-lane state (checkpoint / resume): mrp_state_words() 32-bit words per lane. */
 int mrp_state_words(int env_id);
 int mrp_get_state(mrp_ctx* ctx, uint32_t* out /* [n_lanes][state_words] */);
@@ -196,6 +215,9 @@ const char* mrp_norm_last_error(const mrp_norm* n);
 int mrp_norm_set_stream(mrp_norm* n, void* hip_stream);   /* as mrp_set_stream: NULL = the HIP null stream */
 /* VecNormalize.training: statistics update on (1) or frozen (0, evaluation) */
 int mrp_norm_set_training(mrp_norm* n, int training);
+/* VecNormalize.norm_obs: with 0 the observation statistics are not updated (SB3 updates obs_rms
+ * only when training and norm_obs); the normalised outputs are still written */
+int mrp_norm_set_norm_obs(mrp_norm* n, int norm_obs);
 /* VecNormalize.reset: update obs statistics, normalise obs, zero the discounted returns and
  * the Monitor accumulators */
 int mrp_norm_reset_device(mrp_norm* n, const float* d_obs, float* d_obs_out);

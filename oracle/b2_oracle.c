@@ -243,7 +243,7 @@ static void tree_init(Tree* t) {
     t->nodes = (TreeNode*)calloc((size_t)t->nodeCapacity, sizeof(TreeNode));
     for (int i = 0; i < t->nodeCapacity - 1; ++i) { t->nodes[i].parent = i + 1; t->nodes[i].height = -1; }
     t->nodes[t->nodeCapacity - 1].parent = NULLN; t->nodes[t->nodeCapacity - 1].height = -1;
-    t->freeList = 0; t->insertionCount = 0;
+    t->freeList = 0; t->insertionCount = 0; t->maxId = -1;
 }
 static int tree_alloc(Tree* t) {
     if (t->freeList == NULLN) {
@@ -261,6 +261,7 @@ static int tree_alloc(Tree* t) {
     t->nodes[id].parent = NULLN; t->nodes[id].child1 = NULLN; t->nodes[id].child2 = NULLN;
     t->nodes[id].height = 0; t->nodes[id].userData = NULL;
     ++t->nodeCount;
+    if (id > t->maxId) t->maxId = id;
     return id;
 }
 static void tree_free(Tree* t, int id) {
@@ -439,6 +440,7 @@ static void bp_init(BroadPhase* bp) {
 static void bp_buffer_move(BroadPhase* bp, int id) {
     if (bp->moveCount == bp->moveCap) { bp->moveCap *= 2; bp->moveBuf = (int*)realloc(bp->moveBuf, sizeof(int) * (size_t)bp->moveCap); }
     bp->moveBuf[bp->moveCount++] = id;
+    if (bp->moveCount > bp->maxMove) bp->maxMove = bp->moveCount;
 }
 static void bp_unbuffer_move(BroadPhase* bp, int id) {
     for (int i = 0; i < bp->moveCount; ++i) if (bp->moveBuf[i] == id) bp->moveBuf[i] = NULLN;
@@ -666,6 +668,7 @@ static void cm_add_pair(ContactManager* cm, Fixture* fixtureA, Fixture* fixtureB
     bodyB->contactList = &c->nodeB;
     bodyA->flags |= BF_AWAKE; bodyB->flags |= BF_AWAKE;
     ++cm->contactCount;
+    if (cm->contactCount > cm->maxContacts) cm->maxContacts = cm->contactCount;
 }
 
 static void cm_find_new_contacts(ContactManager* cm) {
@@ -1623,6 +1626,8 @@ static void world_solve(World* w, TimeStep step) {
                 other->flags |= BF_ISLAND;
             }
         }
+        if (is.bodyCount > w->maxIslandBodies) w->maxIslandBodies = is.bodyCount;
+        if (is.contactCount > w->maxIslandContacts) w->maxIslandContacts = is.contactCount;
         island_solve(&is, w, step);
         for (int i = 0; i < is.bodyCount; ++i) {
             Body* b = is.bodies[i];
@@ -1731,6 +1736,8 @@ static void world_solve_toi(World* w, TimeStep step) {
         sub.positionIterations = 20;
         sub.velocityIterations = step.velocityIterations;
         sub.warmStarting = 0;
+        if (is.bodyCount > w->maxToiIslandBodies) w->maxToiIslandBodies = is.bodyCount;
+        if (is.contactCount > w->maxToiIslandContacts) w->maxToiIslandContacts = is.contactCount;
         island_solve_toi(&is, sub, bA->islandIndex, bB->islandIndex);
         for (int i = 0; i < is.bodyCount; ++i) {
             Body* body = is.bodies[i];
@@ -1753,6 +1760,7 @@ void b2o_step(World* w, float dt, int velIters, int posIters) {
     step.dtRatio = w->inv_dt0 * dt;
     step.warmStarting = 1;
     cm_collide(&w->cm);
+    for (Contact* c = w->cm.contactList; c; c = c->next) w->touching += (c->flags & CF_TOUCHING) != 0;
     if (w->stepComplete && step.dt > 0.0f) world_solve(w, step);
     if (step.dt > 0.0f) world_solve_toi(w, step);
     if (step.dt > 0.0f) w->inv_dt0 = step.inv_dt;

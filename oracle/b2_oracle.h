@@ -89,11 +89,11 @@ typedef struct {
     AABB aabb; void* userData; int parent; /* == next in free list */
     int child1, child2, height;
 } TreeNode;
-typedef struct { int root; TreeNode* nodes; int nodeCount, nodeCapacity, freeList, insertionCount; } Tree;
+typedef struct { int root; TreeNode* nodes; int nodeCount, nodeCapacity, freeList, insertionCount; int maxId; } Tree;
 typedef struct { int a, b; } Pair;
 typedef struct {
     Tree tree; int proxyCount;
-    int* moveBuf; int moveCap, moveCount;
+    int* moveBuf; int moveCap, moveCount, maxMove;
     Pair* pairBuf; int pairCap, pairCount;
     int queryProxyId;
 } BroadPhase;
@@ -101,7 +101,7 @@ typedef struct {
 typedef void (*ContactCb)(void* ctx, Contact* c);
 typedef struct {
     BroadPhase bp;
-    Contact* contactList; int contactCount;
+    Contact* contactList; int contactCount, maxContacts;
     ContactCb begin, end; void* listenerCtx;   /* NULL begin/end == no listener */
 } ContactManager;
 
@@ -115,6 +115,10 @@ typedef struct World {
     V2 gravity;
     /* diagnostics */
     long toiEvents, posIters, velIters;
+    long touching;      /* touching contacts after each Step's Collide, summed (the device's counter) */
+    /* capacity high-water marks (test infrastructure: the device keeps fixed per-lane pools,
+     * tests/test_oracle.py checks these stay inside them) */
+    int maxIslandBodies, maxIslandContacts, maxToiIslandBodies, maxToiIslandContacts;
 } World;
 
 typedef struct { int type; V2 position; float angle; float linearDamping, angularDamping; int tag; } BodyDef;

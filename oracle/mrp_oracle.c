@@ -673,6 +673,15 @@ void or_get_flags(const OrEnv* e, int* gc, int* bip) {
 }
 int or_contact_count(const OrEnv* e) { return e->world->cm.contactCount; }
 void or_counters(const OrEnv* e, long* toi, long* pos) { *toi = e->world->toiEvents; *pos = e->world->posIters; }
+void or_capacity(const OrEnv* e, int* out8) {
+    const World* w = e->world;
+    out8[0] = w->cm.maxContacts; out8[1] = w->cm.bp.tree.maxId; out8[2] = w->cm.bp.maxMove;
+    out8[3] = w->maxIslandBodies; out8[4] = w->maxIslandContacts; out8[5] = w->maxToiIslandBodies;
+    out8[6] = w->maxToiIslandContacts; out8[7] = w->cm.bp.tree.nodeCapacity;
+}
+void or_counters_ex(const OrEnv* e, long* out3) {
+    out3[0] = e->world->toiEvents; out3[1] = e->world->posIters; out3[2] = e->world->touching;
+}
 long or_vel_constraint_iters(const OrEnv* e) { return e->world->velIters; }
 static int push_proxies(const Body* b, int* out, int k) {
     /* creation order == reverse fixture-list order */
@@ -711,9 +720,24 @@ int or_body_mass(const OrEnv* e, int i, float* out4) {
  * max_steps <= 0 uses the registered TimeLimit.  bodies [n_lanes][6*(n_blocks+n_agents)] final state, rsum [n_lanes] summed float32(reward),
  * resets [n_lanes] episodes started. */
 #include <omp.h>
+static long batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_t lane_offset, const double* lo,
+                      const double* hi, int max_steps, int threads, double* seconds, float* bodies, double* rsum,
+                      int* resets, int* caps);
 long or_batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_t lane_offset, const double* lo,
                   const double* hi, int max_steps, int threads, double* seconds, float* bodies, double* rsum,
                   int* resets) {
+    return batch_run(env_id, n_lanes, steps, seed, lane_offset, lo, hi, max_steps, threads, seconds, bodies, rsum, resets,
+                     NULL);
+}
+long or_batch_capacity(int env_id, int n_lanes, int steps, uint64_t seed, const double* lo, const double* hi, int max_steps,
+                       int threads, int* caps8) {
+    double sec;
+    for (int k = 0; k < 8; ++k) caps8[k] = 0;
+    return batch_run(env_id, n_lanes, steps, seed, 0, lo, hi, max_steps, threads, &sec, NULL, NULL, NULL, caps8);
+}
+static long batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_t lane_offset, const double* lo,
+                      const double* hi, int max_steps, int threads, double* seconds, float* bodies, double* rsum,
+                      int* resets, int* caps) {
     if (!valid(env_id) || n_lanes <= 0 || steps < 0) return -1;
     const Cfg cfg = CFGS[env_id];
     const int limit = max_steps > 0 ? max_steps : cfg.max_steps;
@@ -737,7 +761,9 @@ long or_batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_t la
         }
 #pragma omp single
         t0 = omp_get_wtime();
-#pragma omp for schedule(static) reduction(+:total)
+        /* dynamic: a lane's cost varies by orders of magnitude between steps (contact islands), and
+         * lanes are independent, so the CPU baseline takes the best balance it can */
+#pragma omp for schedule(dynamic, 4) reduction(+:total)
         for (int l = 0; l < n_lanes; ++l) {
             OrEnv* e = envs[l];
             const uint64_t g = lane_offset + (uint64_t)l;
@@ -767,6 +793,12 @@ long or_batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_t la
         for (int l = 0; l < n_lanes; ++l) {
             if (bodies) or_get_bodies(envs[l], bodies + (size_t)l * nbody);
             if (resets) resets[l] = episode[l];
+            if (caps) {
+                int c[8];
+                or_capacity(envs[l], c);
+#pragma omp critical
+                for (int k = 0; k < 8; ++k) if (c[k] > caps[k]) caps[k] = c[k];
+            }
             or_destroy(envs[l]);
         }
     }

@@ -41,12 +41,22 @@ int or_get_bodies(const OrEnv* e, float* out);
 void or_get_flags(const OrEnv* e, int* goal_contact, int* blks_in_place);
 int or_contact_count(const OrEnv* e);
 void or_counters(const OrEnv* e, long* toi_events, long* pos_iters);
+/* toi events, position iterations, touching contacts after each Step's Collide (summed) */
+void or_counters_ex(const OrEnv* e, long* out3);
 /* proxy ids of all fixtures in creation order (blocks, agents, walls) */
 int or_proxy_ids(const OrEnv* e, int* out);
 int or_body_mass(const OrEnv* e, int i, float* out4);
 long or_batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_t lane_offset, const double* lo,
                   const double* hi, int max_steps, int threads, double* seconds, float* bodies, double* rsum,
                   int* resets);
+
+/* capacity high-water marks of one lane since creation: max live contacts, max tree node id,
+ * max move-buffer fill, max island bodies / contacts, max TOI-island bodies / contacts, tree node
+ * capacity (the device keeps fixed pools per lane; tests check these stay inside them) */
+void or_capacity(const OrEnv* e, int* out8);
+/* or_batch_run's workload, returning the capacity maxima over all lanes in caps8 */
+long or_batch_capacity(int env_id, int n_lanes, int steps, uint64_t seed, const double* lo, const double* hi, int max_steps,
+                       int threads, int* caps8);
 
 /* glibc-faithful math exported for tests */
 float or_sinf(float x);

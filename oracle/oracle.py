@@ -60,6 +60,7 @@ def lib():
         L.or_contact_count.argtypes = [P]
         L.or_contact_count.restype = c_int
         L.or_counters.argtypes = [P, P, P]
+        L.or_counters_ex.argtypes = [P, P]
         L.or_proxy_ids.argtypes = [P, P]
         L.or_proxy_ids.restype = c_int
         L.or_sinf.argtypes = [c_float]
@@ -74,6 +75,9 @@ def lib():
         L.or_body_mass.restype = c_int
         L.or_batch_run.argtypes = [c_int, c_int, c_int, ctypes.c_uint64, ctypes.c_uint64, P, P, c_int, c_int, P, P, P, P]
         L.or_batch_run.restype = ctypes.c_long
+        L.or_batch_capacity.argtypes = [c_int, c_int, c_int, ctypes.c_uint64, P, P, c_int, c_int, P]
+        L.or_batch_capacity.restype = ctypes.c_long
+        L.or_capacity.argtypes = [P, P]
         _lib = L
     return _lib
 
@@ -142,6 +146,11 @@ class OracleEnv:
         lib().or_counters(self._h, _ptr(a), _ptr(b))
         return int(a[0]), int(b[0])
 
+    def counters_ex(self) -> dict:
+        out = np.zeros(3, np.int64)
+        lib().or_counters_ex(self._h, _ptr(out))
+        return {"toi_events": int(out[0]), "position_iterations": int(out[1]), "touching_contacts": int(out[2])}
+
     def body_mass(self, i: int):
         """(mass, inertia about the body origin, local centre x, y) of dynamic body i."""
         out = np.zeros(4, np.float32)
@@ -181,3 +190,18 @@ def batch_run(env_id: int, lanes: int, steps: int, seed: int, bounds, threads: i
     if outputs:
         return int(n), float(sec[0]), bodies, rsum, eps
     return int(n), float(sec[0])
+
+
+CAPACITY_NAMES = ("contacts", "tree_node_id", "move_buffer", "island_bodies", "island_contacts", "toi_island_bodies",
+                  "toi_island_contacts", "tree_node_capacity")
+
+
+def batch_capacity(env_id: int, lanes: int, steps: int, seed: int, bounds, threads: int = 1, max_steps: int = 0) -> dict:
+    """batch_run's workload; returns the per-lane capacity high-water marks (max over lanes)."""
+    lo = np.ascontiguousarray([b[0] for b in bounds], dtype=np.float64)
+    hi = np.ascontiguousarray([b[1] for b in bounds], dtype=np.float64)
+    caps = np.zeros(8, np.int32)
+    n = lib().or_batch_capacity(env_id, lanes, steps, seed, _ptr(lo), _ptr(hi), max_steps, threads, _ptr(caps))
+    if n < 0:
+        raise ValueError("or_batch_capacity: bad arguments")
+    return dict(zip(CAPACITY_NAMES, (int(c) for c in caps)))

@@ -42,7 +42,8 @@ class RunningMeanStd:
 
 class VecNormalizeRef:
     def __init__(self, n_lanes: int, obs_dim: int, clip_obs=10.0, clip_reward=10.0, gamma=0.99, epsilon=1e-8,
-                 training: bool = True):
+                 training: bool = True, norm_obs: bool = True):
+        self.norm_obs = norm_obs   # SB3: the observation statistics move only when training and norm_obs
         self.obs_rms = RunningMeanStd((obs_dim,))
         self.ret_rms = RunningMeanStd(())
         self.clip_obs, self.clip_reward, self.gamma, self.epsilon = clip_obs, clip_reward, gamma, epsilon
@@ -60,7 +61,7 @@ class VecNormalizeRef:
         return np.clip(x, -self.clip_reward, self.clip_reward).astype(np.float32)
 
     def reset(self, obs):
-        if self.training:
+        if self.training and self.norm_obs:
             self.obs_rms.update(obs)
         self.returns[:] = 0.0
         self.ep_ret[:] = 0.0
@@ -70,7 +71,7 @@ class VecNormalizeRef:
     def step(self, obs, reward, done, term_obs=None):
         """Returns (obs', reward', term_obs' for done lanes or None, episode returns, lengths for done lanes)."""
         done = np.asarray(done).astype(bool)
-        if self.training:
+        if self.training and self.norm_obs:
             self.obs_rms.update(obs)
         o = self.normalize_obs(obs)
         if self.training:

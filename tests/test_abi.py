@@ -97,3 +97,21 @@ def test_product_never_imports_the_oracle():
                 src = open(os.path.join(dirpath, f)).read()
                 assert not re.search(r"^\s*(from|import)\s+oracle", src, flags=re.M), f
                 assert "mrp_oracle" not in src and "libmrp_oracle" not in src, f
+
+
+def test_lane_layout_restatement_matches_library(lib):
+    """tests/lane_layout.py (the LaneState word offsets the fault-injection GPU tests write
+    through mrp_set_state) sizes every env's lane exactly as the library does."""
+    from lane_layout import offsets
+    for e in range(7):
+        off, words = offsets(e)
+        assert words == lib.mrp_state_words(e), e
+        assert off["nonfinite"] + 2 <= words and off["fault"] < off["agent_dist"]
+
+
+def test_status_flag_bits_agree():
+    src = open(HEADER).read()
+    from gym_puzzles_amd import _native
+    assert f"#define MRP_STATUS_NONFINITE 0x{_native.STATUS_NONFINITE:x}" in src
+    assert f"#define MRP_STATUS_FAULT 0x{_native.STATUS_FAULT:x}" in src
+    assert f"#define MRP_STATUS_KIND_MASK 0x{_native.STATUS_KIND_MASK:x}" in src

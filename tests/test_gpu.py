@@ -74,6 +74,13 @@ def test_step_parity_host_inputs(gpu_lib, orc, env_id):
     pos = sum(o.counters()[1] for o in envs)
     assert b.counters() == (toi, pos)
     assert not b.faults().any(), "a loop guard tripped"
+    # per-batch counters (mrp_counters_ex) against the oracle's
+    ctr = b.counters_ex()
+    oc = [o.counters_ex() for o in envs]
+    assert ctr["toi_events"] == toi and ctr["position_iterations"] == pos
+    assert ctr["touching_contacts"] == sum(c["touching_contacts"] for c in oc) > 0
+    assert ctr["steps"] == lanes * steps
+    assert ctr["nonfinite_steps"] == 0 and ctr["faulted_lanes"] == 0
     b.close()
 
 
@@ -313,3 +320,118 @@ def test_whole_episode_soak(gpu_lib, orc, env_id):
     _eq("bodies", b.bodies(), bodies)
     _eq("reward sums", rsum, orsum)
     b.close()
+
+
+def _twin(env_id, lanes, seed=21, warm=30):
+    """Two identical batches advanced `warm` device-RNG steps (auto-reset on)."""
+    from gym_puzzles_amd import Batch
+    bs = [Batch(env_id, lanes, seed=seed) for _ in range(2)]
+    for b in bs:
+        b.set_auto_reset(True)
+        b.reset()
+        for _ in range(warm):
+            b.step()
+    return bs
+
+
+@pytest.mark.parametrize("env_id", [0, 4])
+def test_nonfinite_lane_is_flagged_not_fatal(gpu_lib, env_id):
+    """A lane corrupted through mrp_set_state (a NaN body velocity) is reported by the status
+    flag MRP_STATUS_NONFINITE and counted; the other lanes stay bit-identical to an uncorrupted
+    twin batch and nothing raises (SURVEY.md 8b Errors: per-lane NaN -> info['nan'], never a crash)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from gym_puzzles_amd._native import STATUS_NONFINITE
+    from lane_layout import offsets
+    lanes, bad = 64, 5
+    a, b = _twin(env_id, lanes)
+    st = b.get_state().copy()
+    off, _ = offsets(env_id)
+    st[bad, off["vx"]] = np.float32(np.nan).view(np.uint32)
+    b.set_state(st)
+    flagged = 0
+    keep = np.arange(lanes) != bad
+    for t in range(3):
+        oa, ra, da, _ = a.step()
+        ob, rb, db, _ = b.step()
+        if t == 0:   # the NaN velocity reaches the position and the observation in this step
+            assert b.status[bad] & STATUS_NONFINITE
+        flagged += int(bool(b.status[bad] & STATUS_NONFINITE))
+        assert not (b.status[keep] & STATUS_NONFINITE).any()
+        _eq("obs of healthy lanes", ob[keep], oa[keep])
+        _eq("reward of healthy lanes", rb[keep], ra[keep])
+    # NaN compares false, so the reference's in-place test `not abs(fx - x) > eps` holds and the
+    # lane ends its episode (auto-reset) -- the flag counts the lane-steps that carried the NaN
+    assert b.counters_ex()["nonfinite_steps"] == flagged >= 1 and a.counters_ex()["nonfinite_steps"] == 0
+
+
+def test_loop_guard_fault_reaches_info(gpu_lib):
+    """A lane whose loop-guard fault word is set (as a tripped guard leaves it; written through
+    mrp_set_state) is reported in every later step: status bit MRP_STATUS_FAULT and the VecEnv's
+    info['mrp_fault'] = the guard code; no other lane is flagged and every lane's physics is
+    bit-identical to an uncorrupted twin (the fault word is a report, not a physics input)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from gym_puzzles_amd import MultiRobotPuzzleVecEnv
+    from gym_puzzles_amd._native import STATUS_FAULT
+    from lane_layout import offsets
+    lanes, bad = 64, 9
+    venvs = [MultiRobotPuzzleVecEnv(0, lanes, seed=3) for _ in range(2)]
+    for v in venvs:
+        v.reset()
+    rs = np.random.RandomState(2)
+    acts = rs.uniform(-1, 1, size=(30, lanes, 6)).astype(np.float32)
+    for t in range(20):
+        for v in venvs:
+            v.step(acts[t])
+    st = venvs[1].batch.get_state().copy()
+    off, _ = offsets(0)
+    st[bad, off["fault"]] = np.uint32(4)          # MRP_FAULT_CONTACT_LIST
+    venvs[1].batch.set_state(st)
+    for t in range(20, 24):
+        oa, ra, da, ia = venvs[0].step(acts[t])
+        ob, rb, db, ib = venvs[1].step(acts[t])
+        assert venvs[1].batch.status[bad] & STATUS_FAULT
+        assert ib[bad].get("mrp_fault") == 4
+        assert all("mrp_fault" not in ib[i] for i in range(lanes) if i != bad)
+        assert all("mrp_fault" not in x for x in ia)
+        _eq("obs", ob, oa)
+        _eq("reward", rb, ra)
+    assert venvs[1].batch.counters_ex()["faulted_lanes"] == 1
+    for v in venvs:
+        v.close()
+
+
+@pytest.mark.parametrize("env_id", [0, 2, 4])
+def test_multi_step_launch_equals_single_steps(gpu_lib, env_id):
+    """mrp_step_n_device (K env steps per launch, device-RNG actions, auto-reset) writes every
+    step's obs / reward / done / truncated / status / terminal obs bit-identical to K single-step
+    launches, and leaves the identical lane state."""
+    import torch
+    lanes, K, rounds = 256, 8, 5
+    a, b = _twin(env_id, lanes, seed=31, warm=3)
+    for x in (a, b):
+        x.set_time_limit(13)
+    dev = torch.device("cuda", 0)
+    O = a.obs_dim
+    z = lambda *s, dt=torch.float32: torch.zeros(s, dtype=dt, device=dev)  # noqa: E731
+    obs, rew, r64, done, tr, stt, term = (z(K, lanes, O), z(K, lanes), z(K, lanes, dt=torch.float64),
+                                          z(K, lanes, dt=torch.uint8), z(K, lanes, dt=torch.uint8),
+                                          z(K, lanes, dt=torch.uint8), z(K, lanes, O))
+    a.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    for r in range(rounds):
+        a.step_n_device(K, 0, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), tr.data_ptr(), stt.data_ptr(),
+                        term.data_ptr(), r64.data_ptr())
+        torch.cuda.synchronize()
+        for k in range(K):
+            ob, rb, db, tb = b.step(want_terminal_obs=True)
+            _eq(f"obs@{r},{k}", obs[k].cpu().numpy(), ob)
+            _eq(f"reward@{r},{k}", rew[k].cpu().numpy(), rb)
+            _eq(f"reward64@{r},{k}", r64[k].cpu().numpy(), b.reward64)
+            _eq(f"done@{r},{k}", done[k].cpu().numpy(), db)
+            _eq(f"truncated@{r},{k}", tr[k].cpu().numpy(), tb)
+            _eq(f"status@{r},{k}", stt[k].cpu().numpy(), b.status)
+            m = db.astype(bool)
+            _eq(f"terminal obs@{r},{k}", term[k].cpu().numpy()[m], b.terminal_obs[m])
+    _eq("state", a.get_state(), b.get_state())
+    assert a.counters_ex() == b.counters_ex()

@@ -9,6 +9,8 @@ sequential float64 sums of the same float32 rewards in the same order: bit-exact
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import pytest
 
@@ -171,8 +173,9 @@ def test_vecnormalize_save_load_and_eval_flags(gpu_lib, tmp_path):
     env.reset()
     for _ in range(30):
         env.step(act())
-    path = str(tmp_path / "saved_env.npz")
+    path = str(tmp_path / "saved_env.pkl")   # train.py:149 / test.py:66 use this exact name
     env.save(path)
+    assert os.path.exists(path) and not os.path.exists(path + ".npz")
     st = env.get_stats()
     env.close()
 
@@ -193,3 +196,54 @@ def test_vecnormalize_save_load_and_eval_flags(gpu_lib, tmp_path):
     o, r, d, infos = ev.step(act())
     np.testing.assert_array_equal(o, ev.get_original_obs())
     ev.close()
+
+
+def test_restatement_norm_obs_off_freezes_obs_statistics():
+    """SB3 VecNormalize updates obs_rms only when training and norm_obs; the returns' statistics
+    still move with norm_obs off."""
+    from oracle.vecnorm_ref import VecNormalizeRef
+    rs = np.random.RandomState(2)
+    n = VecNormalizeRef(8, 3, norm_obs=False)
+    n.reset(rs.normal(size=(8, 3)))
+    for _ in range(5):
+        n.step(rs.normal(size=(8, 3)), rs.normal(size=8), np.zeros(8, bool))
+    np.testing.assert_array_equal(n.obs_rms.mean, np.zeros(3))
+    np.testing.assert_array_equal(n.obs_rms.var, np.ones(3))
+    assert n.obs_rms.count == 1e-4 and n.ret_rms.count > 1
+
+
+@pytest.mark.gpu
+def test_device_norm_obs_off_matches_restatement(gpu_lib):
+    """norm_obs=False on the device: obs statistics frozen, returns' statistics as SB3's."""
+    import torch
+
+    from gym_puzzles_amd import Batch, DeviceVecNormalize
+    from oracle.vecnorm_ref import VecNormalizeRef
+    lanes, steps = 128, 30
+    dev = torch.device("cuda", 0)
+    b = Batch(0, lanes, seed=4)
+    b.set_auto_reset(True)
+    b.set_time_limit(15)
+    O = b.obs_dim
+    norm = DeviceVecNormalize(lanes, O, 0)
+    norm.norm_obs = False
+    ref = VecNormalizeRef(lanes, O, norm_obs=False)
+    o0 = b.reset().copy()
+    nobs = torch.zeros((lanes, O), device=dev)
+    norm.reset(torch.from_numpy(o0).to(dev), nobs)
+    ref.reset(o0)
+    z = lambda *s, dt=torch.float32: torch.zeros(s, dtype=dt, device=dev)  # noqa: E731
+    obs, rew, done, nrew = z(lanes, O), z(lanes), z(lanes, dt=torch.uint8), z(lanes)
+    b.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    for _ in range(steps):
+        b.step_device(0, obs.data_ptr(), rew.data_ptr(), done.data_ptr())
+        norm.step(obs, rew, done, nobs, nrew)
+        ref.step(obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy())
+    st = norm.get_stats()
+    np.testing.assert_array_equal(st["obs_mean"], np.zeros(O))
+    np.testing.assert_array_equal(st["obs_var"], np.ones(O))
+    assert st["obs_count"] == 1e-4
+    np.testing.assert_allclose([st["ret_mean"], st["ret_var"], st["ret_count"]],
+                               [ref.ret_rms.mean, ref.ret_rms.var, ref.ret_rms.count], rtol=1e-10)
+    norm.close()
+    b.close()

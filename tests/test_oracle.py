@@ -343,3 +343,45 @@ def test_batch_run_lane_offset_invariance(orc):
     _, _, half, rs_half, ep_half = orc.batch_run(0, 4, 120, 17, b, threads=1, lane_offset=4, outputs=True)
     assert np.array_equal(full[4:], half) and np.array_equal(rs_full[4:], rs_half)
     assert np.array_equal(ep_full[4:], ep_half)
+
+
+# The device keeps every per-lane structure in a fixed pool (gym_puzzles_amd/csrc/mrp_config.h,
+# mrp_world.h LaneState / Shared): contact slots CMAX, tree nodes tree_n (the moved-proxy set is a
+# 32-bit mask), move buffer MOVE_N, island arrays NBODY = ND + 4 bodies and CMAX contacts (the
+# register / lane solvers need <= 64).  Box2D grows these dynamically; the oracle does too and
+# records its high-water marks, so a long synthetic rollout shows the fixed pools are never
+# exceeded (an overrun on the device would corrupt the lane's LDS instead of failing).
+POOLS = {e: {"contacts": c, "tree_node_id": (16 if 2 * nf - 1 <= 16 else 32) - 1, "move_buffer": 16,
+             "island_bodies": na + nb + 4, "island_contacts": min(c, 64), "toi_island_bodies": na + nb + 4,
+             "toi_island_contacts": min(c, 32)}
+         for e, (na, nb, nf, c) in {0: (2, 1, 8, 21), 1: (5, 1, 11, 48), 2: (2, 1, 12, 53), 3: (2, 1, 12, 53),
+                                    4: (2, 3, 15, 91), 5: (2, 1, 8, 21), 6: (2, 1, 8, 21)}.items()}
+
+
+@pytest.mark.parametrize("env_id", range(7))
+def test_device_pools_hold_the_oracle_high_water_marks(oracle_lib, env_id):
+    from gym_puzzles_amd.spawn import draw_bounds
+    from oracle.oracle import batch_capacity
+    caps = batch_capacity(env_id, 1024, 300, 41, draw_bounds(env_id), threads=min(8, os.cpu_count() or 1), max_steps=60)
+    for k, lim in POOLS[env_id].items():
+        assert caps[k] <= lim, (k, caps[k], lim)
+    assert caps["tree_node_id"] < 32 and caps["move_buffer"] >= 1 and caps["contacts"] >= 1
+
+
+@pytest.mark.parametrize("env_id", range(7))
+def test_oracle_under_asan_ubsan(env_id):
+    """The oracle's sources built with AddressSanitizer + UBSan (make -C oracle asan, every finding
+    fatal) run the synthetic workload of every env id cleanly: 64 lanes x 500 steps, TimeLimit 60
+    (8 resets per lane)."""
+    import subprocess
+    from gym_puzzles_amd.spawn import draw_bounds
+    here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")
+    subprocess.run(["make", "-s", "-C", here, "asan"], check=True)
+    args = [repr(float(x)) for lo, hi in draw_bounds(env_id) for x in (lo, hi)]
+    r = subprocess.run([os.path.join(here, "build", "oracle_check_asan"), str(env_id), "64", "500", "60"] + args,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    caps = json.loads(r.stdout)
+    assert caps["env_steps"] == 64 * 500
+    for k, lim in POOLS[env_id].items():
+        assert caps[k] <= lim, (k, caps[k], lim)

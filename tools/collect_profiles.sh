@@ -12,6 +12,8 @@ for k in "${!ENVS[@]}"; do
   python3 tools/traffic.py $D/fetch $D/write $1 $2 profiles/pmc_traffic.json
   cp "$(find $D/kt -name '*kernel_stats.csv' -print -quit)" profiles/${R}_${k}_kernel_stats.csv
   grep -h '"metric"' $D/kt.log > profiles/${R}_${k}_bench_under_rocprof.json
+  python3 tools/kt_window.py "$(find $D/kt -name '*kernel_trace.csv' -print -quit)" ${WARMUP:-10} ${STEPS:-100} \
+      profiles/${R}_${k}_bench_under_rocprof.json > profiles/${R}_${k}_kernel_window.json
 done
 grep -h '"metric"' gpurun_out/bench_default.log > profiles/${R}_bench_default.json
 grep -h '"metric"' gpurun_out/bench_driver.log > profiles/${R}_bench_driver_window.json
