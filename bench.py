@@ -115,6 +115,28 @@ def single_env_rate(env_name: str, steps: int = 300) -> dict:
             "path": f"gym_puzzles_amd.make('{env_name}').step(): 1-lane kernel + host copies per call"}
 
 
+def load_valu_latency(env_id: int, lanes: int, first: int, last: int, seed: int, kern_ms: float):
+    """roofline.valu / roofline.latency: the oracle op-count model of exactly this workload
+    (tools/roofline_model.py -> profiles/r3_valu_latency.json, keyed by env, lanes, timed step
+    window and seed) over the live kernel_ms; None when the table has no entry for this run."""
+    path = os.path.join(HERE, "profiles", "r3_valu_latency.json")
+    try:
+        with open(path) as f:
+            m = json.load(f)[f"{env_id}:{lanes}:{first}:{last}:{seed}"]
+    except (OSError, ValueError, KeyError):
+        return None, None
+    peak = m["constants"]["valu_peak_flops"]
+    ach = m["flops_per_launch"] / (kern_ms * 1e-3)
+    valu = {"achieved": ach / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s", "frac": ach / peak,
+            "flops_per_launch": m["flops_per_launch"],
+            "source": "oracle op counts of this exact workload (tools/roofline_model.py, profiles/r3_valu_latency.json)"}
+    lat = {"floor_ms": m["latency_floor_ms"], "kernel_ms": kern_ms, "frac": m["latency_floor_ms"] / kern_ms,
+           "slowest_lane_dependent_ops": m["slowest_lane_dependent_ops_per_launch"],
+           "model": "mean over the timed launches of the slowest lane's dependent solver ops (velocity updates, position "
+                    "points) x 6 cycles (tools/micro/latbench.hip) / 2.4 GHz; serial LDS phases and TOI bookkeeping not counted"}
+    return valu, lat
+
+
 def load_traffic(env_id: int, lanes: int):
     """HBM bytes per k_step launch from the committed rocprofv3 PMC pass (profiles/), or None."""
     path = os.path.join(HERE, "profiles", "pmc_traffic.json")
@@ -354,6 +376,7 @@ def main():
         algo_bytes = ALGO_BYTES[args.env] * L
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
         traffic = load_traffic(args.env, L)
+        valu, latency = load_valu_latency(args.env, L, args.warmup + 1, args.warmup + K, args.seed, kern_ms)
         line = {
             "metric": "env-steps/sec (whole node) at N envs/GPU",
             "value": value,
@@ -379,7 +402,8 @@ def main():
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "limiter": "latency: the serial Gauss-Seidel chains (velocity sweeps, position passes, TOI) of "
                                     "the slowest lanes, one wave's VALU issue; not HBM and not MFMA",
-                         "note": "HBM fraction reported because the north star asks for it (SURVEY.md 8d)"},
+                         "note": "HBM fraction reported because the north star asks for it (SURVEY.md 8d)",
+                         "valu": valu, "latency": latency},
             "checks": dict(bad, ok=checks_ok),
             "diagnostics": {"counters": ctr,
                             "timed_steps_after_spawn": [args.warmup + 1, args.warmup + K],

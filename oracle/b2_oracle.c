@@ -610,6 +610,7 @@ static void contact_update(Contact* c, ContactManager* cm) {
     int wasTouching = (c->flags & CF_TOUCHING) == CF_TOUCHING;
     Body* bA = c->fA->body; Body* bB = c->fB->body;
     collide_polygons(&c->manifold, &c->fA->shape, bA->xf, &c->fB->shape, bB->xf);
+    cm->satCalls++;
     int touching = c->manifold.pointCount > 0;
     for (int i = 0; i < c->manifold.pointCount; ++i) {
         MPoint* mp2 = c->manifold.points + i;
@@ -1238,6 +1239,96 @@ static void integrate_positions(Island* is, float h, int syncBodies) {
     }
 }
 
+/* ---- work model (OrWork, test infrastructure): device sweep counts and dependency levels ---- */
+/* dependency levels of the island's Gauss-Seidel order: contact i waits for the last earlier
+ * contact that shares one of its dynamic bodies (`dyn[k]`: island body k moves under this solve);
+ * returns the level count, and the sum over levels of each level's largest point count */
+static int work_levels(const Solver* s, const int* dyn, int* level_points) {
+    int last[256], lvmax_pts[256];
+    int nb = 0;
+    for (int i = 0; i < s->count; ++i) {
+        const int a = s->vcs[i].indexA, b = s->vcs[i].indexB;
+        if (a + 1 > nb) nb = a + 1;
+        if (b + 1 > nb) nb = b + 1;
+    }
+    for (int k = 0; k < nb && k < 256; ++k) last[k] = 0;
+    int L = 0;
+    for (int i = 0; i < s->count && i < 256; ++i) {
+        const int a = s->vcs[i].indexA, b = s->vcs[i].indexB;
+        int lv = 1;
+        if (dyn[a] && last[a] + 1 > lv) lv = last[a] + 1;
+        if (dyn[b] && last[b] + 1 > lv) lv = last[b] + 1;
+        if (dyn[a]) last[a] = lv;
+        if (dyn[b]) last[b] = lv;
+        if (lv > L) { for (int k = L; k < lv; ++k) lvmax_pts[k] = 0; L = lv; }
+        if (s->pcs[i].pointCount > lvmax_pts[lv - 1]) lvmax_pts[lv - 1] = s->pcs[i].pointCount;
+    }
+    int lp = 0;
+    for (int k = 0; k < L; ++k) lp += lvmax_pts[k];
+    if (level_points) *level_points = lp;
+    return L;
+}
+/* critical path of `reps` repetitions of the island's Gauss-Seidel order, each contact lasting
+ * its point count (by_points) or 1: a contact starts when the previous contacts that share one of
+ * its dynamic bodies have finished (the sweeps unrolled, so sweep k+1 may overlap sweep k) */
+static long work_pipe(const Solver* s, const int* dyn, int reps, int by_points) {
+    long fin[256];
+    int nb = 0;
+    for (int i = 0; i < s->count; ++i) {
+        if (s->vcs[i].indexA + 1 > nb) nb = s->vcs[i].indexA + 1;
+        if (s->vcs[i].indexB + 1 > nb) nb = s->vcs[i].indexB + 1;
+    }
+    for (int k = 0; k < nb && k < 256; ++k) fin[k] = 0;
+    long end = 0;
+    for (int r = 0; r < reps; ++r)
+        for (int i = 0; i < s->count; ++i) {
+            const int a = s->vcs[i].indexA, b = s->vcs[i].indexB;
+            long t = 0;
+            if (dyn[a] && fin[a] > t) t = fin[a];
+            if (dyn[b] && fin[b] > t) t = fin[b];
+            t += by_points ? s->pcs[i].pointCount : 1;
+            if (dyn[a]) fin[a] = t;
+            if (dyn[b]) fin[b] = t;
+            if (t > end) end = t;
+        }
+    return end;
+}
+/* the velocity sweeps with the device's exact early-exit count: the sweep loop always runs all
+ * `iters` (results are the reference's), the return value is the number the device runs */
+static int work_velocity_sweeps(Solver* s, int iters, int nbodies) {
+    const int nc = s->count, ns = 4 * nc + 3 * nbodies;
+    float* snap = (float*)malloc(sizeof(float) * (size_t)(ns > 0 ? ns : 1));
+    float* cur = (float*)malloc(sizeof(float) * (size_t)(ns > 0 ? ns : 1));
+#define WORK_STATE(dst) do {                                                                       \
+        int k_ = 0;                                                                                \
+        for (int i_ = 0; i_ < nc; ++i_)                                                            \
+            for (int j_ = 0; j_ < 2; ++j_) {                                                       \
+                (dst)[k_++] = s->vcs[i_].points[j_].normalImpulse;                                 \
+                (dst)[k_++] = s->vcs[i_].points[j_].tangentImpulse;                                \
+            }                                                                                      \
+        for (int b_ = 0; b_ < nbodies; ++b_) {                                                     \
+            (dst)[k_++] = s->velocities[b_].v.x; (dst)[k_++] = s->velocities[b_].v.y;              \
+            (dst)[k_++] = s->velocities[b_].w;                                                     \
+        }                                                                                          \
+    } while (0)
+    int have = (iters & 3) == 2, run = -1;
+    if (have) WORK_STATE(snap);
+    for (int it = 0; it < iters; ++it) {
+        solver_solve_velocity(s);
+        if (run >= 0) continue;
+        const int left = iters - (it + 1);
+        if ((left & 3) == 0 && have) {
+            WORK_STATE(cur);
+            if (memcmp(cur, snap, sizeof(float) * (size_t)ns) == 0) run = it + 1;
+        }
+        if ((left & 3) == 2) { WORK_STATE(snap); have = 1; }
+    }
+#undef WORK_STATE
+    free(snap);
+    free(cur);
+    return run >= 0 ? run : iters;
+}
+
 static void island_solve(Island* is, World* w, TimeStep step) {
     float h = step.dt;
     for (int i = 0; i < is->bodyCount; ++i) {
@@ -1260,13 +1351,27 @@ static void island_solve(Island* is, World* w, TimeStep step) {
     solver_init(&s, step, is->contacts, is->contactCount, is->positions, is->velocities);
     solver_init_velocity_constraints(&s);
     if (step.warmStarting) solver_warm_start(&s);
-    for (int i = 0; i < step.velocityIterations; ++i) solver_solve_velocity(&s);
+    const int sweeps = work_velocity_sweeps(&s, step.velocityIterations, is->bodyCount);
     w->velIters += (long)step.velocityIterations * is->contactCount;
     solver_store_impulses(&s);
     integrate_positions(is, h, 0);
+    int passes = 0;
     for (int i = 0; i < step.positionIterations; ++i) {
         w->posIters++;
+        ++passes;
         if (solver_solve_position(&s, 0, -1, -1)) break;
+    }
+    if (is->contactCount > 0) {
+        int dyn[256], lp = 0, pts = 0, n1 = 0, n2 = 0;
+        for (int k = 0; k < is->bodyCount && k < 256; ++k) dyn[k] = is->bodies[k]->invMass > 0.0f || is->bodies[k]->invI > 0.0f;
+        const int L = work_levels(&s, dyn, &lp);
+        for (int i = 0; i < s.count; ++i) { pts += s.pcs[i].pointCount; if (s.vcs[i].pointCount == 2) ++n2; else ++n1; }
+        OrWork* k = &w->work;
+        k->islands += 1; k->vel_sweeps += sweeps;
+        k->vel_upd1 += (long)sweeps * n1; k->vel_upd2 += (long)sweeps * n2; k->vel_levels += (long)sweeps * L;
+        k->pos_passes += passes; k->pos_points += (long)passes * pts; k->pos_level_points += (long)passes * lp;
+        k->vel_pipe += work_pipe(&s, dyn, sweeps, 0);
+        k->pos_pipe += work_pipe(&s, dyn, passes, 1);
     }
     for (int i = 0; i < is->bodyCount; ++i) {
         Body* body = is->bodies[i];
@@ -1277,7 +1382,7 @@ static void island_solve(Island* is, World* w, TimeStep step) {
     solver_free(&s);
 }
 
-static void island_solve_toi(Island* is, TimeStep sub, int toiIndexA, int toiIndexB) {
+static void island_solve_toi(Island* is, TimeStep sub, int toiIndexA, int toiIndexB, OrWork* k) {
     for (int i = 0; i < is->bodyCount; ++i) {
         Body* b = is->bodies[i];
         is->positions[i].c = b->sweep.c; is->positions[i].a = b->sweep.a;
@@ -1285,15 +1390,32 @@ static void island_solve_toi(Island* is, TimeStep sub, int toiIndexA, int toiInd
     }
     Solver s;
     solver_init(&s, sub, is->contacts, is->contactCount, is->positions, is->velocities);
+    int passes = 0;
     for (int i = 0; i < sub.positionIterations; ++i) {
+        ++passes;
         if (solver_solve_position(&s, 1, toiIndexA, toiIndexB)) break;
+    }
+    {   /* work model: in the TOI position passes only the TOI pair moves */
+        int dyn[256], lp = 0, pts = 0;
+        for (int q = 0; q < is->bodyCount && q < 256; ++q) dyn[q] = q == toiIndexA || q == toiIndexB;
+        work_levels(&s, dyn, &lp);
+        for (int i = 0; i < s.count; ++i) pts += s.pcs[i].pointCount;
+        k->toi_pos_points += (long)passes * pts; k->toi_pos_level_points += (long)passes * lp;
+        k->pos_pipe += work_pipe(&s, dyn, passes, 1);
     }
     is->bodies[toiIndexA]->sweep.c0 = is->positions[toiIndexA].c;
     is->bodies[toiIndexA]->sweep.a0 = is->positions[toiIndexA].a;
     is->bodies[toiIndexB]->sweep.c0 = is->positions[toiIndexB].c;
     is->bodies[toiIndexB]->sweep.a0 = is->positions[toiIndexB].a;
     solver_init_velocity_constraints(&s);
-    for (int i = 0; i < sub.velocityIterations; ++i) solver_solve_velocity(&s);
+    const int sweeps = work_velocity_sweeps(&s, sub.velocityIterations, is->bodyCount);
+    {
+        int dyn[256];
+        for (int q = 0; q < is->bodyCount && q < 256; ++q) dyn[q] = is->bodies[q]->invMass > 0.0f || is->bodies[q]->invI > 0.0f;
+        const int L = work_levels(&s, dyn, NULL);
+        k->toi_vel_upd += (long)sweeps * s.count; k->toi_vel_levels += (long)sweeps * L;
+        k->vel_pipe += work_pipe(&s, dyn, sweeps, 0);
+    }
     integrate_positions(is, sub.dt, 1);
     solver_free(&s);
 }
@@ -1678,6 +1800,7 @@ static void world_solve_toi(World* w, TimeStep step) {
                 DProxy pB = { fB->shape.v, fB->shape.count, fB->shape.radius };
                 int state; float beta;
                 time_of_impact(&state, &beta, &pA, &pB, bA->sweep, bB->sweep, 1.0f);
+                w->work.toi_calls++;
                 if (state == TOI_TOUCHING) alpha = fmin_(alpha0 + (1.0f - alpha0) * beta, 1.0f);
                 else alpha = 1.0f;
                 c->toi = alpha;
@@ -1738,7 +1861,7 @@ static void world_solve_toi(World* w, TimeStep step) {
         sub.warmStarting = 0;
         if (is.bodyCount > w->maxToiIslandBodies) w->maxToiIslandBodies = is.bodyCount;
         if (is.contactCount > w->maxToiIslandContacts) w->maxToiIslandContacts = is.contactCount;
-        island_solve_toi(&is, sub, bA->islandIndex, bB->islandIndex);
+        island_solve_toi(&is, sub, bA->islandIndex, bB->islandIndex, &w->work);
         for (int i = 0; i < is.bodyCount; ++i) {
             Body* body = is.bodies[i];
             body->flags &= ~BF_ISLAND;

@@ -102,8 +102,30 @@ typedef void (*ContactCb)(void* ctx, Contact* c);
 typedef struct {
     BroadPhase bp;
     Contact* contactList; int contactCount, maxContacts;
+    long satCalls;      /* work model: b2CollidePolygons calls (contact updates) */
     ContactCb begin, end; void* listenerCtx;   /* NULL begin/end == no listener */
 } ContactManager;
+
+/* Work model (test infrastructure, tools/chain_model.py): the serial solver work one lane's
+ * step carries as the device runs it -- velocity sweeps counted with the device's exact early exit
+ * (mrp_world.h solver_velocity_*: state after sweep k equals the state after k-2) -- and the same
+ * work grouped into dependency levels (consecutive Gauss-Seidel contacts whose dynamic bodies are
+ * disjoint commute bit-exactly).  Counts accumulate from world creation. */
+typedef struct {
+    long islands;                        /* discrete islands with >= 1 contact */
+    long vel_sweeps;                     /* velocity sweeps run */
+    long vel_upd1, vel_upd2;             /* contact updates run, 1- / 2-point */
+    long vel_levels;                     /* sweeps run x dependency levels of the island */
+    long pos_passes, pos_points;         /* position passes, point updates */
+    long pos_level_points;               /* passes x sum over levels of the level's largest point count */
+    long toi_vel_upd, toi_vel_levels;    /* the same for TOI islands */
+    long toi_pos_points, toi_pos_level_points;
+    long sat_calls, toi_calls;           /* narrow-phase polygon pairs, b2TimeOfImpact calls */
+    long vel_pipe;                       /* critical path of the velocity sweeps (discrete + TOI islands) unrolled
+                                          * over all sweeps run: contacts of sweep k+1 may start once the
+                                          * contacts they share dynamic bodies with have finished */
+    long pos_pipe;                       /* the same for the position passes, weighted by point count */
+} OrWork;
 
 enum { WF_NEWFIXTURE = 1, WF_LOCKED = 2, WF_CLEARFORCES = 4 };
 typedef struct World {
@@ -119,6 +141,7 @@ typedef struct World {
     /* capacity high-water marks (test infrastructure: the device keeps fixed per-lane pools,
      * tests/test_oracle.py checks these stay inside them) */
     int maxIslandBodies, maxIslandContacts, maxToiIslandBodies, maxToiIslandContacts;
+    OrWork work;
 } World;
 
 typedef struct { int type; V2 position; float angle; float linearDamping, angularDamping; int tag; } BodyDef;

@@ -679,6 +679,12 @@ void or_capacity(const OrEnv* e, int* out8) {
     out8[3] = w->maxIslandBodies; out8[4] = w->maxIslandContacts; out8[5] = w->maxToiIslandBodies;
     out8[6] = w->maxToiIslandContacts; out8[7] = w->cm.bp.tree.nodeCapacity;
 }
+void or_work(const OrEnv* e, long* out16) {
+    OrWork k = e->world->work;
+    k.sat_calls = e->world->cm.satCalls;
+    const long* v = (const long*)&k;
+    for (int i = 0; i < 16; ++i) out16[i] = v[i];
+}
 void or_counters_ex(const OrEnv* e, long* out3) {
     out3[0] = e->world->toiEvents; out3[1] = e->world->posIters; out3[2] = e->world->touching;
 }
@@ -722,22 +728,27 @@ int or_body_mass(const OrEnv* e, int i, float* out4) {
 #include <omp.h>
 static long batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_t lane_offset, const double* lo,
                       const double* hi, int max_steps, int threads, double* seconds, float* bodies, double* rsum,
-                      int* resets, int* caps);
+                      int* resets, int* caps, long* work);
 long or_batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_t lane_offset, const double* lo,
                   const double* hi, int max_steps, int threads, double* seconds, float* bodies, double* rsum,
                   int* resets) {
     return batch_run(env_id, n_lanes, steps, seed, lane_offset, lo, hi, max_steps, threads, seconds, bodies, rsum, resets,
-                     NULL);
+                     NULL, NULL);
 }
 long or_batch_capacity(int env_id, int n_lanes, int steps, uint64_t seed, const double* lo, const double* hi, int max_steps,
                        int threads, int* caps8) {
     double sec;
     for (int k = 0; k < 8; ++k) caps8[k] = 0;
-    return batch_run(env_id, n_lanes, steps, seed, 0, lo, hi, max_steps, threads, &sec, NULL, NULL, NULL, caps8);
+    return batch_run(env_id, n_lanes, steps, seed, 0, lo, hi, max_steps, threads, &sec, NULL, NULL, NULL, caps8, NULL);
+}
+long or_batch_work(int env_id, int n_lanes, int steps, uint64_t seed, const double* lo, const double* hi, int max_steps,
+                   int threads, long* work) {
+    double sec;
+    return batch_run(env_id, n_lanes, steps, seed, 0, lo, hi, max_steps, threads, &sec, NULL, NULL, NULL, NULL, work);
 }
 static long batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_t lane_offset, const double* lo,
                       const double* hi, int max_steps, int threads, double* seconds, float* bodies, double* rsum,
-                      int* resets, int* caps) {
+                      int* resets, int* caps, long* work) {
     if (!valid(env_id) || n_lanes <= 0 || steps < 0) return -1;
     const Cfg cfg = CFGS[env_id];
     const int limit = max_steps > 0 ? max_steps : cfg.max_steps;
@@ -772,6 +783,8 @@ static long batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_
             for (int s = 0; s < steps; ++s) {
                 for (int j = 0; j < cfg.act_dim; ++j)
                     act[j] = (float)(-1.0 + 2.0 * or_rng_u01(seed, g, 3, (uint64_t)s * 64 + (uint64_t)j));
+                long w0[16];
+                if (work) or_work(e, w0);
                 or_step(e, act, obs, &rew, &done, &kind);
                 rs += (double)(float)rew;
                 ++total;
@@ -783,6 +796,11 @@ static long batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_
                     or_reset(e, draws, act, obs);
                     ++episode[l];
                     elapsed = 0;
+                }
+                if (work) {   /* this launch's work for the lane: the step plus an auto-reset's own step */
+                    long w1[16];
+                    or_work(e, w1);
+                    for (int k = 0; k < 16; ++k) work[((size_t)s * n_lanes + l) * 16 + k] = w1[k] - w0[k];
                 }
             }
             if (rsum) rsum[l] = rs;

@@ -78,6 +78,9 @@ def lib():
         L.or_batch_capacity.argtypes = [c_int, c_int, c_int, ctypes.c_uint64, P, P, c_int, c_int, P]
         L.or_batch_capacity.restype = ctypes.c_long
         L.or_capacity.argtypes = [P, P]
+        L.or_work.argtypes = [P, P]
+        L.or_batch_work.argtypes = [c_int, c_int, c_int, ctypes.c_uint64, P, P, c_int, c_int, P]
+        L.or_batch_work.restype = ctypes.c_long
         _lib = L
     return _lib
 
@@ -205,3 +208,19 @@ def batch_capacity(env_id: int, lanes: int, steps: int, seed: int, bounds, threa
     if n < 0:
         raise ValueError("or_batch_capacity: bad arguments")
     return dict(zip(CAPACITY_NAMES, (int(c) for c in caps)))
+
+
+WORK_NAMES = ("islands", "vel_sweeps", "vel_upd1", "vel_upd2", "vel_levels", "pos_passes", "pos_points",
+              "pos_level_points", "toi_vel_upd", "toi_vel_levels", "toi_pos_points", "toi_pos_level_points",
+              "sat_calls", "toi_calls", "vel_pipe", "pos_pipe")
+
+
+def batch_work(env_id: int, lanes: int, steps: int, seed: int, bounds, threads: int = 1, max_steps: int = 0) -> np.ndarray:
+    """batch_run's workload; returns int64 [steps, lanes, 16]: each launch's work per lane (WORK_NAMES)."""
+    lo = np.ascontiguousarray([b[0] for b in bounds], dtype=np.float64)
+    hi = np.ascontiguousarray([b[1] for b in bounds], dtype=np.float64)
+    out = np.zeros((steps, lanes, 16), np.int64)
+    n = lib().or_batch_work(env_id, lanes, steps, seed, _ptr(lo), _ptr(hi), max_steps, threads, _ptr(out))
+    if n < 0:
+        raise ValueError("or_batch_work: bad arguments")
+    return out

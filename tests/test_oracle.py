@@ -385,3 +385,25 @@ def test_oracle_under_asan_ubsan(env_id):
     assert caps["env_steps"] == 64 * 500
     for k, lim in POOLS[env_id].items():
         assert caps[k] <= lim, (k, caps[k], lim)
+
+
+def test_work_model_is_consistent(oracle_lib):
+    """The oracle's work model (OrWork; tools/chain_model.py, tools/roofline_model.py): sweeps run
+    never exceed 180 per island (the device's exact early exit only shortens), dependency levels and
+    the unrolled critical path never exceed the contact-by-contact count, and the committed
+    VALU/latency table holds the bench's default and driver-window keys."""
+    from gym_puzzles_amd.spawn import draw_bounds
+    from oracle.oracle import WORK_NAMES, batch_work
+    W = {n: i for i, n in enumerate(WORK_NAMES)}
+    w = batch_work(0, 256, 40, 17, draw_bounds(0), threads=min(8, os.cpu_count() or 1))
+    t = w.sum(axis=(0, 1))
+    assert 0 < t[W["vel_sweeps"]] <= 180 * t[W["islands"]]
+    upd = t[W["vel_upd1"]] + t[W["vel_upd2"]]
+    assert t[W["vel_levels"]] <= upd and t[W["vel_pipe"]] <= upd + t[W["toi_vel_upd"]]
+    assert t[W["pos_level_points"]] <= t[W["pos_points"]] and t[W["pos_passes"]] <= 60 * t[W["islands"]]
+    assert (w >= 0).all()
+    with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                           "r3_valu_latency.json")) as f:
+        table = json.load(f)
+    for key in ("0:4096:6:25:17", "0:4096:21:220:17"):
+        assert table[key]["flops_per_launch"] > 0 and table[key]["latency_floor_ms"] > 0

@@ -18,6 +18,10 @@ ARGS="--steps $STEPS --warmup $WARMUP --no-cpu-baseline --later-window 0 --episo
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 bench.py $ARGS > $OUT/kt.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- python3 bench.py $ARGS > $OUT/write.log 2>&1
+if [ -n "${VALU_PMC:-}" ]; then   # VALU / SALU instruction counts and busy cycles (one pass, SQ block only)
+  timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVES --output-format csv -d $OUT/valu -o valu \
+      -- python3 bench.py $ARGS > $OUT/valu.log 2>&1
+fi
 python3 tools/traffic.py $OUT/fetch $OUT/write $ENV $LANES profiles/pmc_traffic.json
 cp "$(find $OUT/kt -name '*kernel_stats.csv' -print -quit)" profiles/${TAG}_kernel_stats.csv
 grep -h "\"metric\"" $OUT/kt.log > profiles/${TAG}_bench_under_rocprof.json
