@@ -10,7 +10,7 @@ for rep in 1 2; do
     [[ "$spec" == *:* ]] && mode=${spec##*:}
     for cfg in "20 5" "200 20"; do
       read -r K W <<< "$cfg"
-      r=$(MRP_LIB=$lib timeout -k 5 120 python bench.py --steps $K --warmup $W --no-cpu-baseline --later-window 0 --schedule $mode 2>/dev/null | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('%.3fM' % (d['value']/1e6), 'kernel %.3f ms' % d['roofline']['kernel_ms'])") || { echo "bench failed for $spec"; exit 1; }
+      r=$(MRP_LIB=$lib timeout -k 5 120 python bench.py --steps $K --warmup $W --no-cpu-baseline --later-window 0 --episode 0 --multi-step 0 --single-env 0 --schedule $mode 2>/dev/null | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('%.3fM' % (d['value']/1e6), 'kernel %.3f ms' % d['roofline']['kernel_ms'])") || { echo "bench failed for $spec"; exit 1; }
       echo "$spec steps=$K warmup=$W: $r" | tee -a $out
     done
   done
