@@ -164,6 +164,10 @@ int mrp_create(int env_id, int n_lanes, int device, uint64_t seed, uint64_t lane
     EnvTables tables;
     if (!build_tables(env_id, tables)) { g_create_error = "bad env_id"; return MRP_E_ARG; }
     if (n_lanes <= 0) { g_create_error = "n_lanes must be > 0"; return MRP_E_ARG; }
+    // the velocity solver drops the (then identically +0) restitution velocity bias (mrp_world.h CC):
+    // every fixture of every env has the default restitution 0 (no reference fixtureDef sets one)
+    for (int f = 0; f < tables.n_fix; ++f)
+        if (tables.fix_restitution[f] != 0.0f) { g_create_error = "fixture restitution != 0 is not supported"; return MRP_E_ARG; }
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev <= 0) {

@@ -1080,7 +1080,10 @@ template <int ENV> struct World {
     // v_pk_* instruction for both halves of a b2Vec2 operation) and the impulses (the state).
     struct CC {
         P2 rA0, rB0, rA1, rB1;   // arms of points 0 and 1, stored as pperp(r) = (-r.y, r.x) (see pcrossp)
-        P2 normal, vbias, k01, k13, nm01, nm13;   // K = [k0 k1; k1 k3], K^-1 = [nm0 nm1; nm1 nm3]
+        P2 normal, k01, k13, nm01, nm13;   // K = [k0 k1; k1 k3], K^-1 = [nm0 nm1; nm1 nm3]
+        // no velocity bias: every fixture of these envs has restitution 0 (checked at mrp_create), so
+        // SolveVelocityConstraints' velocityBias is -0 * vRel = +0 or the initial +0, and vn - (+0) == vn
+        // bit for bit (-0 - +0 = -0): the subtraction is dropped, not approximated
         P2 mA, mB;   // (mA, mA), (mB, mB): broadcast once, not re-splatted (and hoisted into extra pairs) per use
         float nmass0, nmass1, tmass0, tmass1, iA, iB, friction;
         int pcount;
@@ -1091,7 +1094,6 @@ template <int ENV> struct World {
         o.rA0 = p2(-c.rAy[0], c.rAx[0]); o.rB0 = p2(-c.rBy[0], c.rBx[0]);
         o.rA1 = p2(-c.rAy[1], c.rAx[1]); o.rB1 = p2(-c.rBy[1], c.rBx[1]);
         o.normal = p2(c.nx, c.ny);
-        o.vbias = p2(c.vbias[0], c.vbias[1]);
         o.k01 = p2(c.k0, c.k1); o.k13 = p2(c.k1, c.k3); o.nm01 = p2(c.nm0, c.nm1); o.nm13 = p2(c.nm1, c.nm3);
         o.nmass0 = c.nmass[0]; o.nmass1 = c.nmass[1]; o.tmass0 = c.tmass[0]; o.tmass1 = c.tmass[1];
         o.mA = pbc(c.mA); o.iA = c.iA; o.mB = pbc(c.mB); o.iB = c.iB; o.friction = c.friction;
@@ -1105,9 +1107,20 @@ template <int ENV> struct World {
     // `pcount` is wave-uniform; `pick(c)` turns the block solver's per-lane case condition into the
     // wave-uniform decision (uni: identical lanes; lane_bit: lane i's).  Reads the impulses from
     // c.ni / c.ti and returns the new ones in ni / ti (the caller decides which lanes keep them).
+    // runtime point count (the lanes path: contact i's count, wave-uniform): one branch to the
+    // compile-time forms
     template <class Pick>
     __device__ __forceinline__ static void vel_update(const CC& c, int pcount, Pick pick, P2& ni, P2& ti,
                                                           P2& vA, float& wA, P2& vB, float& wB) {
+        if (pcount == 2) vel_update_t<2>(c, pick, ni, ti, vA, wA, vB, wB);
+        else vel_update_t<1>(c, pick, ni, ti, vA, wA, vB, wB);
+    }
+    // PCOUNT = the contact's manifold point count, a template parameter so every branch on it is
+    // resolved at compile time (straight-line update, no phi copies between point-count paths)
+    template <int PCOUNT, class Pick>
+    __device__ __forceinline__ static void vel_update_t(const CC& c, Pick pick, P2& ni, P2& ti,
+                                                            P2& vA, float& wA, P2& vB, float& wB) {
+        constexpr int pcount = PCOUNT;
         const P2 mA = c.mA, mB = c.mB;
         const float iA = c.iA, iB = c.iB;
         // tangent = b2Cross(normal, 1.0f) = (1*n.y, -1*n.x) = (n.y, -n.x) exactly: a half swap and a
@@ -1145,7 +1158,7 @@ template <int ENV> struct World {
         if (pcount == 1) {
             const P2 dv = ((vB + (pbc(wB) * c.rB0)) - vA) - (pbc(wA) * c.rA0);
             const float vn = pdot(dv, normal);
-            float lambda = -c.nmass0 * (vn - c.vbias.x);
+            float lambda = -c.nmass0 * vn;   // vn - velocityBias, velocityBias == +0 (see CC)
             const float newImpulse = fmax_(ni.x + lambda, 0.0f);
             lambda = newImpulse - ni.x;
             ni.x = newImpulse;
@@ -1159,8 +1172,8 @@ template <int ENV> struct World {
             const P2 dv1 = ((vB + (pbc(wB) * c.rB0)) - vA) - (pbc(wA) * c.rA0);
             const P2 dv2 = ((vB + (pbc(wB) * c.rB1)) - vA) - (pbc(wA) * c.rA1);
             float vn1 = pdot(dv1, normal), vn2 = pdot(dv2, normal);
-            // b = (vn1 - vbias0, vn2 - vbias1) - (k0*a.x + k2*a.y, k1*a.x + k3*a.y), k2 = k1
-            P2 b = p2(vn1, vn2) - c.vbias;
+            // b = (vn1 - vbias0, vn2 - vbias1) - (k0*a.x + k2*a.y, k1*a.x + k3*a.y), k2 = k1, vbias == +0
+            P2 b = p2(vn1, vn2);
             b = b - (c.k01 * pbc(a.x) + c.k13 * pbc(a.y));
             // x = -(nm0*b.x + nm2*b.y, nm1*b.x + nm3*b.y), nm2 = nm1
             P2 x = -(c.nm01 * pbc(b.x) + c.nm13 * pbc(b.y));
@@ -1190,13 +1203,14 @@ template <int ENV> struct World {
         }
     }
     // the register-resident form: identical lanes, every lane keeps the result
+    template <int PC>
     __device__ __forceinline__ static void cc_update(CC& c, P2& vA, float& wA, P2& vB, float& wB) {
         // opaque to the optimiser once per update, so values derived from the normal (the tangent,
         // its swapped / negated forms) are formed inside the instructions rather than hoisted out
         // of the sweep loop into registers of their own
         asm volatile("" : "+v"(c.normal));
         P2 ni, ti;
-        vel_update(c, __builtin_amdgcn_readfirstlane(c.pcount), [](bool x) { return uni(x); }, ni, ti, vA, wA, vB, wB);
+        vel_update_t<PC>(c, [](bool x) { return uni(x); }, ni, ti, vA, wA, vB, wB);
         c.ni = ni; c.ti = ti;
     }
     // exact early exit (see solver_velocity_lanes): the state after sweep k is compared with the
@@ -1231,7 +1245,14 @@ template <int ENV> struct World {
         }
     };
     __device__ __forceinline__ static bool snap_initial(int iters) { return (iters & 3) == 2; }   // sweep 0 is a snapshot point
+    // register paths: the contacts' point counts (wave-uniform, fixed for the whole solve) select a
+    // compile-time instantiation of the sweep loop
     __device__ __forceinline__ int solver_velocity_one(Isl& is, VC* vcs, int iters, bool early_exit = true) {
+        return __builtin_amdgcn_readfirstlane(vcs[0].pointCount) == 2 ? sweep_one<2>(is, vcs, iters, early_exit)
+                                                                       : sweep_one<1>(is, vcs, iters, early_exit);
+    }
+    template <int P0>
+    __device__ __forceinline__ int sweep_one(Isl& is, VC* vcs, int iters, bool early_exit) {
         CC c = load_cc(vcs[0]);
         const int ia = vcs[0].iaI, ib = vcs[0].ibI;
         P2 vA = p2(is.vvx[ia], is.vvy[ia]); float wA = is.vw[ia];
@@ -1241,7 +1262,7 @@ template <int ENV> struct World {
         int sweeps = 0;
         for (int it = 0; it < iters; ++it) {
             ++sweeps;
-            cc_update(c, vA, wA, vB, wB);
+            cc_update<P0>(c, vA, wA, vB, wB);
             if (early_exit && ((iters - it - 1) & 1) == 0) {
                 const float cur[10] = {vA.x, vA.y, wA, vB.x, vB.y, wB, c.ni.x, c.ni.y, c.ti.x, c.ti.y};
                 if (snap.step(it, iters, cur)) break;
@@ -1257,7 +1278,7 @@ template <int ENV> struct World {
     // Two contacts: an island of two contacts has three bodies, X shared by both contacts, Y the
     // other body of contact 0 and Z that of contact 1; X's role (A or B) in each contact is a
     // template parameter, so every body access is a register.
-    template <bool XA0, bool XA1>
+    template <bool XA0, bool XA1, int P0, int P1>
     __device__ __forceinline__ int sweep_two(Isl& is, VC* vcs, int iters, bool early_exit, int x, int y, int z) {
         CC c0 = load_cc(vcs[0]), c1 = load_cc(vcs[1]);
         P2 vX = p2(is.vvx[x], is.vvy[x]), vY = p2(is.vvx[y], is.vvy[y]), vZ = p2(is.vvx[z], is.vvy[z]);
@@ -1268,8 +1289,8 @@ template <int ENV> struct World {
         int sweeps = 0;
         for (int it = 0; it < iters; ++it) {
             ++sweeps;
-            if (XA0) cc_update(c0, vX, wX, vY, wY); else cc_update(c0, vY, wY, vX, wX);
-            if (XA1) cc_update(c1, vX, wX, vZ, wZ); else cc_update(c1, vZ, wZ, vX, wX);
+            if (XA0) cc_update<P0>(c0, vX, wX, vY, wY); else cc_update<P0>(c0, vY, wY, vX, wX);
+            if (XA1) cc_update<P1>(c1, vX, wX, vZ, wZ); else cc_update<P1>(c1, vZ, wZ, vX, wX);
             if (early_exit && ((iters - it - 1) & 1) == 0) {
                 const float cur[17] = {vX.x, vX.y, wX, vY.x, vY.y, wY, vZ.x, vZ.y, wZ, c0.ni.x, c0.ni.y, c0.ti.x, c0.ti.y,
                                        c1.ni.x, c1.ni.y, c1.ti.x, c1.ti.y};
@@ -1286,7 +1307,7 @@ template <int ENV> struct World {
     }
     // Two contacts between the same two bodies (e.g. an agent against both boxes of the T block):
     // contact 1 is (P, Q) when SAME, else (Q, P).
-    template <bool SAME>
+    template <bool SAME, int P0, int P1>
     __device__ __forceinline__ int sweep_same(Isl& is, VC* vcs, int iters, bool early_exit, int p, int q) {
         CC c0 = load_cc(vcs[0]), c1 = load_cc(vcs[1]);
         P2 vP = p2(is.vvx[p], is.vvy[p]), vQ = p2(is.vvx[q], is.vvy[q]);
@@ -1296,8 +1317,8 @@ template <int ENV> struct World {
         int sweeps = 0;
         for (int it = 0; it < iters; ++it) {
             ++sweeps;
-            cc_update(c0, vP, wP, vQ, wQ);
-            if (SAME) cc_update(c1, vP, wP, vQ, wQ); else cc_update(c1, vQ, wQ, vP, wP);
+            cc_update<P0>(c0, vP, wP, vQ, wQ);
+            if (SAME) cc_update<P1>(c1, vP, wP, vQ, wQ); else cc_update<P1>(c1, vQ, wQ, vP, wP);
             if (early_exit && ((iters - it - 1) & 1) == 0) {
                 const float cur[14] = {vP.x, vP.y, wP, vQ.x, vQ.y, wQ, c0.ni.x, c0.ni.y, c0.ti.x, c0.ti.y, c1.ni.x, c1.ni.y, c1.ti.x, c1.ti.y};
                 if (snap.step(it, iters, cur)) break;
@@ -1312,15 +1333,23 @@ template <int ENV> struct World {
     }
     // returns -1 when the two contacts share no body (cannot happen inside one island; the caller
     // then uses solver_velocity_lanes)
-    __device__ __forceinline__ int solver_velocity_two(Isl& is, VC* vcs, int iters, bool early_exit = true) {
+    template <int P0, int P1>
+    __device__ __forceinline__ int solver_velocity_two_p(Isl& is, VC* vcs, int iters, bool early_exit) {
         const int a0 = vcs[0].iaI, b0 = vcs[0].ibI, a1 = vcs[1].iaI, b1 = vcs[1].ibI;
-        if (a0 == a1 && b0 == b1) return sweep_same<true>(is, vcs, iters, early_exit, a0, b0);
-        if (a0 == b1 && b0 == a1) return sweep_same<false>(is, vcs, iters, early_exit, a0, b0);
-        if (a0 == a1) return sweep_two<true, true>(is, vcs, iters, early_exit, a0, b0, b1);
-        if (a0 == b1) return sweep_two<true, false>(is, vcs, iters, early_exit, a0, b0, a1);
-        if (b0 == a1) return sweep_two<false, true>(is, vcs, iters, early_exit, b0, a0, b1);
-        if (b0 == b1) return sweep_two<false, false>(is, vcs, iters, early_exit, b0, a0, a1);
+        if (a0 == a1 && b0 == b1) return sweep_same<true, P0, P1>(is, vcs, iters, early_exit, a0, b0);
+        if (a0 == b1 && b0 == a1) return sweep_same<false, P0, P1>(is, vcs, iters, early_exit, a0, b0);
+        if (a0 == a1) return sweep_two<true, true, P0, P1>(is, vcs, iters, early_exit, a0, b0, b1);
+        if (a0 == b1) return sweep_two<true, false, P0, P1>(is, vcs, iters, early_exit, a0, b0, a1);
+        if (b0 == a1) return sweep_two<false, true, P0, P1>(is, vcs, iters, early_exit, b0, a0, b1);
+        if (b0 == b1) return sweep_two<false, false, P0, P1>(is, vcs, iters, early_exit, b0, a0, a1);
         return -1;
+    }
+    __device__ __forceinline__ int solver_velocity_two(Isl& is, VC* vcs, int iters, bool early_exit = true) {
+        const int p0 = __builtin_amdgcn_readfirstlane(vcs[0].pointCount), p1 = __builtin_amdgcn_readfirstlane(vcs[1].pointCount);
+        if (p0 == 2) return p1 == 2 ? solver_velocity_two_p<2, 2>(is, vcs, iters, early_exit)
+                                    : solver_velocity_two_p<2, 1>(is, vcs, iters, early_exit);
+        return p1 == 2 ? solver_velocity_two_p<1, 2>(is, vcs, iters, early_exit)
+                       : solver_velocity_two_p<1, 1>(is, vcs, iters, early_exit);
     }
 
     // ---------------------------------------------------------------- lane-distributed position iterations

@@ -1295,6 +1295,35 @@ static long work_pipe(const Solver* s, const int* dyn, int reps, int by_points) 
 }
 /* the velocity sweeps with the device's exact early-exit count: the sweep loop always runs all
  * `iters` (results are the reference's), the return value is the number the device runs */
+/* diagnostic (b2o_period_diag): for islands whose sweeps never reach period 1 or 2, the earliest
+ * sweep at which the state repeats with ANY period up to 64, histogrammed; [0] islands examined,
+ * [1] of them with no repeat within `iters`, [2 + k] first repeat at sweep k (k < 190), and the
+ * period histogram at [200 + p] */
+static int g_period_diag = 0;
+static long g_period_hist[300];
+void b2o_period_diag(int on, long* out300) {
+    if (out300) for (int i = 0; i < 300; ++i) out300[i] = g_period_hist[i];
+    if (on >= 0) { g_period_diag = on; for (int i = 0; i < 300; ++i) g_period_hist[i] = 0; }
+}
+static int g_model_period = 0;   /* > 0: the work model counts sweeps as if periods up to this were detected */
+void b2o_model_period(int p) { g_model_period = p; }
+static int period_scan(const float* hist, int ns, int iters) {
+    int first = -1, per = 0;
+    const int pmax = g_model_period > 0 ? g_model_period : 64;
+    for (int k = 1; k <= iters && first < 0; ++k)
+        for (int p = 1; p <= pmax && p <= k; ++p)
+            if (memcmp(hist + (size_t)k * ns, hist + (size_t)(k - p) * ns, sizeof(float) * (size_t)ns) == 0) {
+                first = k; per = p; break;
+            }
+#pragma omp critical
+    {
+        g_period_hist[0]++;
+        if (first < 0) g_period_hist[1]++;
+        else { g_period_hist[2 + (first < 190 ? first : 189)]++; g_period_hist[200 + per]++; }
+    }
+    return first;
+}
+
 static int work_velocity_sweeps(Solver* s, int iters, int nbodies) {
     const int nc = s->count, ns = 4 * nc + 3 * nbodies;
     float* snap = (float*)malloc(sizeof(float) * (size_t)(ns > 0 ? ns : 1));
@@ -1313,8 +1342,11 @@ static int work_velocity_sweeps(Solver* s, int iters, int nbodies) {
     } while (0)
     int have = (iters & 3) == 2, run = -1;
     if (have) WORK_STATE(snap);
+    float* hist = (g_period_diag || g_model_period > 0) ? (float*)malloc(sizeof(float) * (size_t)(ns > 0 ? ns : 1) * (size_t)(iters + 1)) : NULL;
+    if (hist) WORK_STATE(hist);
     for (int it = 0; it < iters; ++it) {
         solver_solve_velocity(s);
+        if (hist) WORK_STATE(hist + (size_t)(it + 1) * ns);
         if (run >= 0) continue;
         const int left = iters - (it + 1);
         if ((left & 3) == 0 && have) {
@@ -1324,6 +1356,13 @@ static int work_velocity_sweeps(Solver* s, int iters, int nbodies) {
         if ((left & 3) == 2) { WORK_STATE(snap); have = 1; }
     }
 #undef WORK_STATE
+    if (hist) {
+        if (run < 0 && nc > 0) {
+            const int first = period_scan(hist, ns, iters);
+            if (g_model_period > 0 && first > 0) run = first;
+        }
+        free(hist);
+    }
     free(snap);
     free(cur);
     return run >= 0 ? run : iters;
@@ -1372,6 +1411,10 @@ static void island_solve(Island* is, World* w, TimeStep step) {
         k->pos_passes += passes; k->pos_points += (long)passes * pts; k->pos_level_points += (long)passes * lp;
         k->vel_pipe += work_pipe(&s, dyn, sweeps, 0);
         k->pos_pipe += work_pipe(&s, dyn, passes, 1);
+        const long units = (long)sweeps * s.count + (long)passes * pts;
+        k->isl_units += units;
+        w->stepIslSum += units;
+        if (units > w->stepIslMax) w->stepIslMax = units;
     }
     for (int i = 0; i < is->bodyCount; ++i) {
         Body* body = is->bodies[i];
@@ -1875,6 +1918,7 @@ static void world_solve_toi(World* w, TimeStep step) {
 }
 
 void b2o_step(World* w, float dt, int velIters, int posIters) {
+    w->stepIslSum = 0; w->stepIslMax = 0;
     if (w->flags & WF_NEWFIXTURE) { cm_find_new_contacts(&w->cm); w->flags &= ~WF_NEWFIXTURE; }
     w->flags |= WF_LOCKED;
     TimeStep step;
@@ -1891,4 +1935,5 @@ void b2o_step(World* w, float dt, int velIters, int posIters) {
         for (Body* b = w->bodyList; b; b = b->next) { b->force = v2(0.0f, 0.0f); b->torque = 0.0f; }
     }
     w->flags &= ~WF_LOCKED;
+    w->work.isl_concurrent_save += w->stepIslSum - w->stepIslMax;
 }

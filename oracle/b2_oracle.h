@@ -125,6 +125,10 @@ typedef struct {
                                           * over all sweeps run: contacts of sweep k+1 may start once the
                                           * contacts they share dynamic bodies with have finished */
     long pos_pipe;                       /* the same for the position passes, weighted by point count */
+    long isl_units;                      /* discrete islands' velocity updates + position points */
+    long isl_concurrent_save;            /* per step: those units minus the largest island's (what solving a
+                                          * step's independent islands concurrently would take off the chain) */
+    long reserved[2];
 } OrWork;
 
 enum { WF_NEWFIXTURE = 1, WF_LOCKED = 2, WF_CLEARFORCES = 4 };
@@ -142,6 +146,7 @@ typedef struct World {
      * tests/test_oracle.py checks these stay inside them) */
     int maxIslandBodies, maxIslandContacts, maxToiIslandBodies, maxToiIslandContacts;
     OrWork work;
+    long stepIslSum, stepIslMax;         /* work model: this step's island units, sum and max */
 } World;
 
 typedef struct { int type; V2 position; float angle; float linearDamping, angularDamping; int tag; } BodyDef;
@@ -161,6 +166,12 @@ Fixture* b2o_create_fixture(Body* b, const FixtureDef* def);
 void b2o_destroy_body(World* w, Body* b);
 void b2o_step(World* w, float dt, int velIters, int posIters);
 void b2o_set_listener(World* w, ContactCb begin, ContactCb end, void* ctx);
+
+/* diagnostic: period histogram of the islands whose velocity sweeps never reach period 1 or 2
+ * (see b2_oracle.c); on >= 0 resets and sets the switch, out300 (may be NULL) receives it */
+void b2o_period_diag(int on, long* out300);
+/* diagnostic: the work model counts velocity sweeps as if periods up to p were detected (0 = the device) */
+void b2o_model_period(int p);
 
 /* body API used by the env layer (pybox2d semantics) */
 void b2o_set_linear_velocity(Body* b, V2 v);

@@ -679,11 +679,11 @@ void or_capacity(const OrEnv* e, int* out8) {
     out8[3] = w->maxIslandBodies; out8[4] = w->maxIslandContacts; out8[5] = w->maxToiIslandBodies;
     out8[6] = w->maxToiIslandContacts; out8[7] = w->cm.bp.tree.nodeCapacity;
 }
-void or_work(const OrEnv* e, long* out16) {
+void or_work(const OrEnv* e, long* out20) {
     OrWork k = e->world->work;
     k.sat_calls = e->world->cm.satCalls;
     const long* v = (const long*)&k;
-    for (int i = 0; i < 16; ++i) out16[i] = v[i];
+    for (int i = 0; i < 20; ++i) out20[i] = v[i];
 }
 void or_counters_ex(const OrEnv* e, long* out3) {
     out3[0] = e->world->toiEvents; out3[1] = e->world->posIters; out3[2] = e->world->touching;
@@ -783,7 +783,7 @@ static long batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_
             for (int s = 0; s < steps; ++s) {
                 for (int j = 0; j < cfg.act_dim; ++j)
                     act[j] = (float)(-1.0 + 2.0 * or_rng_u01(seed, g, 3, (uint64_t)s * 64 + (uint64_t)j));
-                long w0[16];
+                long w0[20];
                 if (work) or_work(e, w0);
                 or_step(e, act, obs, &rew, &done, &kind);
                 rs += (double)(float)rew;
@@ -798,9 +798,9 @@ static long batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_
                     elapsed = 0;
                 }
                 if (work) {   /* this launch's work for the lane: the step plus an auto-reset's own step */
-                    long w1[16];
+                    long w1[20];
                     or_work(e, w1);
-                    for (int k = 0; k < 16; ++k) work[((size_t)s * n_lanes + l) * 16 + k] = w1[k] - w0[k];
+                    for (int k = 0; k < 20; ++k) work[((size_t)s * n_lanes + l) * 20 + k] = w1[k] - w0[k];
                 }
             }
             if (rsum) rsum[l] = rs;

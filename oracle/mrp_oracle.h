@@ -58,9 +58,9 @@ void or_capacity(const OrEnv* e, int* out8);
 long or_batch_capacity(int env_id, int n_lanes, int steps, uint64_t seed, const double* lo, const double* hi, int max_steps,
                        int threads, int* caps8);
 
-/* work model (b2_oracle.h OrWork): 16 counters of one lane since creation */
-void or_work(const OrEnv* e, long* out16);
-/* or_batch_run's workload; work[step][lane][16] receives each launch's work per lane */
+/* work model (b2_oracle.h OrWork): 20 counters of one lane since creation */
+void or_work(const OrEnv* e, long* out20);
+/* or_batch_run's workload; work[step][lane][20] receives each launch's work per lane */
 long or_batch_work(int env_id, int n_lanes, int steps, uint64_t seed, const double* lo, const double* hi, int max_steps,
                    int threads, long* work);
 

@@ -212,14 +212,15 @@ def batch_capacity(env_id: int, lanes: int, steps: int, seed: int, bounds, threa
 
 WORK_NAMES = ("islands", "vel_sweeps", "vel_upd1", "vel_upd2", "vel_levels", "pos_passes", "pos_points",
               "pos_level_points", "toi_vel_upd", "toi_vel_levels", "toi_pos_points", "toi_pos_level_points",
-              "sat_calls", "toi_calls", "vel_pipe", "pos_pipe")
+              "sat_calls", "toi_calls", "vel_pipe", "pos_pipe", "isl_units", "isl_concurrent_save", "reserved0",
+              "reserved1")
 
 
 def batch_work(env_id: int, lanes: int, steps: int, seed: int, bounds, threads: int = 1, max_steps: int = 0) -> np.ndarray:
-    """batch_run's workload; returns int64 [steps, lanes, 16]: each launch's work per lane (WORK_NAMES)."""
+    """batch_run's workload; returns int64 [steps, lanes, 20]: each launch's work per lane (WORK_NAMES)."""
     lo = np.ascontiguousarray([b[0] for b in bounds], dtype=np.float64)
     hi = np.ascontiguousarray([b[1] for b in bounds], dtype=np.float64)
-    out = np.zeros((steps, lanes, 16), np.int64)
+    out = np.zeros((steps, lanes, len(WORK_NAMES)), np.int64)
     n = lib().or_batch_work(env_id, lanes, steps, seed, _ptr(lo), _ptr(hi), max_steps, threads, _ptr(out))
     if n < 0:
         raise ValueError("or_batch_work: bad arguments")

@@ -37,8 +37,11 @@ def lane_cycles(w: np.ndarray, mode: str) -> np.ndarray:
     elif mode == "levels":
         vel = w[..., W["vel_levels"]] + w[..., W["toi_vel_levels"]]
         pos = w[..., W["pos_level_points"]] + w[..., W["toi_pos_level_points"]]
-    else:
+    elif mode == "pipe":
         vel, pos = w[..., W["vel_pipe"]], w[..., W["pos_pipe"]]
+    else:   # 'islands': contact order, but a step's independent islands solved concurrently
+        vel = w[..., W["vel_upd1"]] + w[..., W["vel_upd2"]] + w[..., W["toi_vel_upd"]] - w[..., W["isl_concurrent_save"]]
+        pos = w[..., W["pos_points"]] + w[..., W["toi_pos_points"]]
     return C_FIX + C_VEL * vel + C_POS * pos + C_TOI * (w[..., W["toi_vel_upd"]] > 0)
 
 
@@ -48,9 +51,19 @@ def main():
     s0 = int(sys.argv[3]) if len(sys.argv) > 3 else 6
     s1 = int(sys.argv[4]) if len(sys.argv) > 4 else 25
     w = batch_work(env, lanes, s1, 17, draw_bounds(env), threads=os.cpu_count() or 1)
+    if os.environ.get("MODEL_PERIOD"):   # what detecting velocity-sweep periods up to P would take off
+        import ctypes
+        from oracle.oracle import lib
+        lib().b2o_model_period.argtypes = [ctypes.c_int]
+        lib().b2o_model_period(int(os.environ["MODEL_PERIOD"]))
+        wp = batch_work(env, lanes, s1, 17, draw_bounds(env), threads=os.cpu_count() or 1)[s0 - 1:s1]
+        lib().b2o_model_period(0)
+        a, b = lane_cycles(w[s0 - 1:s1], "order").max(axis=1).sum(), lane_cycles(wp, "order").max(axis=1).sum()
+        print(f"period detection up to {os.environ['MODEL_PERIOD']}: slowest-lane sum {a / 1e6:.2f} -> {b / 1e6:.2f} Mcyc (x{a / b:.3f})")
     win = w[s0 - 1:s1]                      # step s (1-based after spawn) = row s - 1
     now, lev, pipe = lane_cycles(win, "order"), lane_cycles(win, "levels"), lane_cycles(win, "pipe")
     mx_now, mx_lev, mx_pipe = now.max(axis=1), lev.max(axis=1), pipe.max(axis=1)
+    mx_isl = lane_cycles(win, "islands").max(axis=1)
     arg = now.argmax(axis=1)
     meas = None
     if len(sys.argv) > 6:
@@ -76,7 +89,8 @@ def main():
         print(line)
     print(f"sum of per-step slowest lanes: contact order {mx_now.sum() / 1e6:.2f} Mcyc, dependency levels "
           f"{mx_lev.sum() / 1e6:.2f} Mcyc (x{mx_now.sum() / mx_lev.sum():.3f}), unrolled critical path "
-          f"{mx_pipe.sum() / 1e6:.2f} Mcyc (x{mx_now.sum() / mx_pipe.sum():.3f})")
+          f"{mx_pipe.sum() / 1e6:.2f} Mcyc (x{mx_now.sum() / mx_pipe.sum():.3f}), independent islands concurrent "
+          f"{mx_isl.sum() / 1e6:.2f} Mcyc (x{mx_now.sum() / mx_isl.sum():.3f})")
     if meas:
         r = np.corrcoef(mx_now, np.array(meas))[0, 1]
         print(f"correlation of the modelled slowest lane with the measured launch time: {r:.3f}; "
