@@ -35,7 +35,7 @@ EXPORTED = (
     "mrp_env_dims", "mrp_create", "mrp_destroy", "mrp_last_error", "mrp_n_lanes", "mrp_env_id",
     "mrp_set_stream", "mrp_synchronize", "mrp_set_reward_params", "mrp_update_params", "mrp_update_goal",
     "mrp_reset", "mrp_reset_device", "mrp_step", "mrp_step_device", "mrp_step_ex", "mrp_step_device_ex",
-    "mrp_step_n_device", "mrp_set_auto_reset", "mrp_set_seed", "mrp_set_schedule",
+    "mrp_step_n_device", "mrp_set_auto_reset", "mrp_set_frameskip", "mrp_set_seed", "mrp_set_schedule",
     "mrp_get_bodies", "mrp_get_flags", "mrp_get_faults", "mrp_counters", "mrp_counters_ex", "mrp_state_words", "mrp_get_state", "mrp_set_state",
     "mrp_set_time_limit", "mrp_selftest_sincos", "mrp_debug_stamps", "mrp_debug_stamps_ext",
     "mrp_debug_trace", "mrp_debug_progress", "mrp_debug_velbench", "mrp_norm_create", "mrp_norm_destroy", "mrp_norm_last_error", "mrp_norm_set_stream",
@@ -84,6 +84,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.mrp_set_seed.argtypes = [P, u64]
     L.mrp_set_schedule.argtypes = [P, i]
     L.mrp_set_auto_reset.argtypes = [P, i]
+    if hasattr(L, "mrp_set_frameskip"):   # absent from libraries built before round 3 (A/B baselines)
+        L.mrp_set_frameskip.argtypes = [P, i]
     L.mrp_get_bodies.argtypes = [P, P]
     L.mrp_get_flags.argtypes = [P, P]
     L.mrp_get_faults.argtypes = [P, P]
@@ -201,6 +203,10 @@ class Batch:
 
     def update_goal(self, epoch, nb_epochs):
         self._check(load().mrp_update_goal(self._h, float(epoch), float(nb_epochs)))
+
+    def set_frameskip(self, frameskip: int):
+        """world.Step calls per env step (MultiRobotPuzzle2(frameskip=k), multi_robot_puzzle_02.py:476-478)."""
+        self._check(load().mrp_set_frameskip(self._h, int(frameskip)))
 
     def set_auto_reset(self, enabled: bool):
         self._check(load().mrp_set_auto_reset(self._h, 1 if enabled else 0))

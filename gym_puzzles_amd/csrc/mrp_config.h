@@ -73,6 +73,8 @@ struct EnvParams {
     double shaped_bounds, shaped_blk_bounds, shaped_puzzle;
     double scaled_epsilon;
     double puzzle_complete;            // v3 puzzle_complete_reward (core.py:155), added as is on completion
+    int frameskip;                     // world.Step calls per env step (multi_robot_puzzle_02.py:139,476-478)
+    int pad;
 };
 
 }  // namespace mrp

@@ -336,7 +336,10 @@ template <int ENV> struct Env : World<ENV> {
         if (tid == 0) apply_actions(sh.act);
         __syncthreads();
         MRP_STAMP(1);
-        this->world_step_coop();
+        // for _ in range(self.frameskip): world.Step(...) (multi_robot_puzzle_02.py:476-478); the
+        // applied forces are cleared by the first Step, as Box2D's autoClearForces does
+        const int fs = P.frameskip > 1 ? P.frameskip : 1;
+        for (int f = 0; f < fs; ++f) this->world_step_coop();
         if (tid == 0) {
             double prevA[NA], prevB[NB];
             for (int i = 0; i < NA; ++i) prevA[i] = S.agent_dist[i];

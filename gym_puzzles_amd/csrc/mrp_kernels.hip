@@ -273,6 +273,12 @@ int mrp_update_goal(mrp_ctx* ctx, double epoch, double nb_epochs) {
     return MRP_OK;
 }
 
+int mrp_set_frameskip(mrp_ctx* ctx, int frameskip) {
+    if (!ctx || frameskip < 1 || frameskip > 64) return MRP_E_ARG;
+    ctx->params.frameskip = frameskip;
+    return MRP_OK;
+}
+
 int mrp_set_auto_reset(mrp_ctx* ctx, int enabled) {
     if (!ctx) return MRP_E_ARG;
     ctx->auto_reset = enabled ? 1 : 0;

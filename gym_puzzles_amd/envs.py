@@ -46,6 +46,8 @@ class _MRPBase:
         self.seed()
         self._b = Batch(self.env_id, 1, device=device)
         self._b.set_time_limit(0)           # gym.wrappers.TimeLimit (make()) owns truncation
+        if getattr(self, "frameskip", 1) != 1:   # world.Step calls per step (multi_robot_puzzle_02.py:476-478)
+            self._b.set_frameskip(self.frameskip)
         self.num_agents = self._b.n_agents
         self.viewer = None
         self.done_status = None
@@ -198,9 +200,14 @@ class MultiRobotPuzzle2(_MRPBase):
     contact_weight = True
 
     def __init__(self, frameskip=1, num_agents=2, device: int = 0):
-        if frameskip != 1 or num_agents != 2:
-            raise NotImplementedError("the device build covers frameskip=1, num_agents=2 (the registered config)")
-        self.frameskip = frameskip
+        # frameskip (multi_robot_puzzle_02.py:139,146,476-478) is a runtime parameter of the device
+        # step; num_agents sizes the obs / action layout and the per-lane pools, which the device
+        # build fixes at compile time per env id: only the registered value 2 has an instantiation
+        if num_agents != 2:
+            raise NotImplementedError("the device build instantiates num_agents=2 (the registered config)")
+        if int(frameskip) < 1:
+            raise ValueError("frameskip must be >= 1")
+        self.frameskip = int(frameskip)
         super().__init__(device)
 
     def _obs_high(self):

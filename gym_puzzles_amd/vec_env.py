@@ -48,13 +48,14 @@ def _lane_flags(batch: Batch, status: np.ndarray, infos: list) -> None:
 
 class MultiRobotPuzzleVecEnv(_VecEnvBase):
     def __init__(self, env_id, num_envs: int, device: int = 0, seed: int = 0, lane_offset: int = 0,
-                 max_episode_steps: int | None = None):
+                 max_episode_steps: int | None = None, frameskip: int = 1):
         self.env_index = _ID[env_id] if isinstance(env_id, str) else int(env_id)
         d = env_dims(self.env_index)
         self.num_envs = num_envs
         self.device = device
         self._seed = seed
         self._lane_offset = lane_offset
+        self.frameskip = int(frameskip)   # MultiRobotPuzzle2(frameskip=k): world.Step calls per env step
         self.observation_space = make_box(-np.inf, np.inf, shape=(d["obs_dim"],), dtype=np.float32)
         self.action_space = make_box(-1.0, 1.0, shape=(d["act_dim"],), dtype=np.float32)
         self.max_episode_steps = d["max_episode_steps"] if max_episode_steps is None else max_episode_steps
@@ -74,6 +75,8 @@ class MultiRobotPuzzleVecEnv(_VecEnvBase):
                         lane_offset=self._lane_offset)
         self._b.set_time_limit(self.max_episode_steps)
         self._b.set_auto_reset(True)
+        if self.frameskip != 1:
+            self._b.set_frameskip(self.frameskip)
 
     # -- VecEnv API ------------------------------------------------------------------------
     def reset(self) -> np.ndarray:

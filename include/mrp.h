@@ -124,6 +124,10 @@ int mrp_step_device_ex(mrp_ctx* ctx, const float* d_actions, float* d_obs, float
 int mrp_step_n_device(mrp_ctx* ctx, int n_steps, const float* d_actions, float* d_obs, float* d_reward, double* d_reward64,
                       uint8_t* d_done, uint8_t* d_truncated, uint8_t* d_status, float* d_terminal_obs);
 int mrp_set_auto_reset(mrp_ctx* ctx, int enabled);
+/* frameskip: world.Step(1/50, 180, 60) calls per env step, 1-64 (default 1).  Replaces the
+ * MultiRobotPuzzle2(frameskip=k) constructor argument (multi_robot_puzzle_02.py:139,146,476-478:
+ * `for _ in range(self.frameskip): self.world.Step(...)`; the reset's extra step takes it too). */
+int mrp_set_frameskip(mrp_ctx* ctx, int frameskip);
 /* Re-key the device counter RNG (spawns of later resets, synthetic actions) without touching the
  * lanes, parameters, stream or time limit: SB3 VecEnv.seed(seed) (train/train.py:63-75 seeds
  * every env before the first reset).  Per-lane streams stay keyed by the global lane index. */

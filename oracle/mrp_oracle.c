@@ -127,6 +127,7 @@ struct OrEnv {
     double w_dAgent, w_agentDist, w_dBlock, w_blkDist;
     double shaped_bounds, shaped_blk_bounds, shaped_puzzle;
     double puzzle_complete;      /* v3 puzzle_complete_reward (core.py:155; step() adds it directly) */
+    int frameskip;               /* world.Step calls per env step (multi_robot_puzzle_02.py:139,476-478) */
 };
 
 /* ContactDetector.BeginContact/EndContact: multi_robot_puzzle_00.py:92-111, _02.py:85-102.
@@ -634,7 +635,9 @@ static void build_obs_and_reward(OrEnv* e, const double* prev_agent, const doubl
 
 void or_step(OrEnv* e, const float* action, double* obs, double* reward, int* done, int* kind) {
     apply_actions(e, action);
-    b2o_step(e->world, 1.0f / 50, 6 * 30, 2 * 30);   /* world.Step(1.0/FPS, 6*30, 2*30) :427-428 */
+    /* for _ in range(self.frameskip): world.Step(1.0/FPS, 6*30, 2*30)  (_02.py:476-478; v0 :427-428 with
+     * frameskip 1 for the low-dim obs, :161-162); forces are cleared after the first Step */
+    for (int f = 0; f < (e->frameskip > 0 ? e->frameskip : 1); ++f) b2o_step(e->world, 1.0f / 50, 6 * 30, 2 * 30);
     double prev_agent[5], prev_block[3];
     memcpy(prev_agent, e->agent_dist, sizeof(prev_agent));
     memcpy(prev_block, e->block_distance, sizeof(prev_block));
@@ -672,6 +675,7 @@ void or_get_flags(const OrEnv* e, int* gc, int* bip) {
     *bip = e->blks_in_place;
 }
 int or_contact_count(const OrEnv* e) { return e->world->cm.contactCount; }
+void or_set_frameskip(OrEnv* e, int frameskip) { e->frameskip = frameskip; }
 void or_counters(const OrEnv* e, long* toi, long* pos) { *toi = e->world->toiEvents; *pos = e->world->posIters; }
 void or_capacity(const OrEnv* e, int* out8) {
     const World* w = e->world;

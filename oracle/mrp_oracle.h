@@ -36,6 +36,8 @@ void or_reset(OrEnv* e, const double* draws, const float* reset_action, double* 
  * (0 none, 1 puzzle complete, 2 agent out of bounds, 3 block out of bounds). */
 void or_step(OrEnv* e, const float* action, double* obs_out, double* reward, int* done, int* kind);
 void or_set_shaped(OrEnv* e, double bounds_penalty, double blk_bounds_penalty, double puzzle_reward);
+/* world.Step calls per env step (MultiRobotPuzzle2(frameskip=k), multi_robot_puzzle_02.py:139,476-478) */
+void or_set_frameskip(OrEnv* e, int frameskip);
 /* dynamic body state in creation order (blocks, then agents): c.x c.y a v.x v.y w */
 int or_get_bodies(const OrEnv* e, float* out);
 void or_get_flags(const OrEnv* e, int* goal_contact, int* blks_in_place);

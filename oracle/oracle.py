@@ -54,6 +54,7 @@ def lib():
         L.or_reset.argtypes = [P, P, P, P]
         L.or_step.argtypes = [P, P, P, P, P, P]
         L.or_set_shaped.argtypes = [P, c_double, c_double, c_double]
+        L.or_set_frameskip.argtypes = [P, c_int]
         L.or_get_bodies.argtypes = [P, P]
         L.or_get_bodies.restype = c_int
         L.or_get_flags.argtypes = [P, P, P]
@@ -125,6 +126,9 @@ class OracleEnv:
         kind = np.zeros(1, np.int32)
         lib().or_step(self._h, _ptr(a), _ptr(obs), _ptr(rew), _ptr(done), _ptr(kind))
         return obs, float(rew[0]), bool(done[0]), int(kind[0])
+
+    def set_frameskip(self, frameskip: int):
+        lib().or_set_frameskip(self._h, int(frameskip))
 
     def set_shaped(self, bounds, blk_bounds, puzzle):
         lib().or_set_shaped(self._h, bounds, blk_bounds, puzzle)

@@ -435,3 +435,39 @@ def test_multi_step_launch_equals_single_steps(gpu_lib, env_id):
             _eq(f"terminal obs@{r},{k}", term[k].cpu().numpy()[m], b.terminal_obs[m])
     _eq("state", a.get_state(), b.get_state())
     assert a.counters_ex() == b.counters_ex()
+
+
+@pytest.mark.parametrize("env_id,frameskip", [(2, 3), (0, 2)])
+def test_frameskip_parity(gpu_lib, orc, env_id, frameskip):
+    """MultiRobotPuzzle2(frameskip=k) (multi_robot_puzzle_02.py:139,476-478): k world.Step calls per
+    env step, bit-identical to the oracle doing the same, including the reset's step."""
+    from gym_puzzles_amd import Batch
+    lanes, steps = 32, 80
+    rs_d = [np.random.RandomState(300 + l) for l in range(lanes)]
+    rs_a = np.random.RandomState(77)
+    b = Batch(env_id, lanes)
+    b.set_frameskip(frameskip)
+    b.update_params(0, 1)
+    envs = [orc.OracleEnv(env_id) for _ in range(lanes)]
+    for o in envs:
+        o.set_frameskip(frameskip)
+        o.set_shaped(1000.0, 100.0, 10000.0)
+    draws = np.stack([reference_draws(env_id, r) for r in rs_d])
+    acts = rs_a.uniform(-1, 1, size=(lanes, b.act_dim)).astype(np.float32)
+    _eq("reset obs", b.reset(draws, acts), np.stack([o.reset(draws[l], acts[l]) for l, o in enumerate(envs)]).astype(np.float32))
+    for t in range(steps):
+        a = rs_a.uniform(-1, 1, size=(lanes, b.act_dim)).astype(np.float32)
+        obs, rew, done, _ = b.step(a)
+        res = [o.step(a[l]) for l, o in enumerate(envs)]
+        _eq(f"obs@{t}", obs, np.stack([r[0] for r in res]).astype(np.float32))
+        _eq(f"reward@{t}", rew, np.array([r[1] for r in res]).astype(np.float32))
+        _eq(f"bodies@{t}", b.bodies(), np.stack([o.bodies() for o in envs]))
+        if done.any():
+            m = done.astype(bool)
+            d2 = np.stack([reference_draws(env_id, r) for r in rs_d])
+            a2 = rs_a.uniform(-1, 1, size=(lanes, b.act_dim)).astype(np.float32)
+            o2 = b.reset(d2, a2, mask=m).copy()
+            for l in np.nonzero(m)[0]:
+                _eq(f"reset obs@{t}", o2[l], envs[l].reset(d2[l], a2[l]).astype(np.float32))
+    assert b.counters()[1] == sum(o.counters()[1] for o in envs)
+    b.close()
