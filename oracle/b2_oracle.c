@@ -1368,6 +1368,38 @@ static int work_velocity_sweeps(Solver* s, int iters, int nbodies) {
     return run >= 0 ? run : iters;
 }
 
+/* diagnostic (b2o_topo_diag): island topologies of 3- and 4-contact islands, weighted by sweeps run:
+ * per contact (A slot, B slot, point count) with body slots numbered by first appearance and static
+ * bodies as slot 7; 64 distinct signatures kept */
+static int g_topo_diag = 0;
+static long g_topo_sig[64], g_topo_w[64];
+static void topo_record(const Solver* s, const Island* is, int sweeps) {
+    int slot[256], ns = 0;
+    for (int k = 0; k < 256; ++k) slot[k] = -1;
+    long sig = s->count;
+    for (int i = 0; i < s->count; ++i) {
+        const int ab[2] = {s->vcs[i].indexA, s->vcs[i].indexB};
+        int sl[2];
+        for (int j = 0; j < 2; ++j) {
+            const Body* b = is->bodies[ab[j]];
+            if (b->invMass == 0.0f && b->invI == 0.0f) { sl[j] = 7; continue; }
+            if (slot[ab[j]] < 0) slot[ab[j]] = ns++;
+            sl[j] = slot[ab[j]];
+        }
+        sig = sig * 1000 + sl[0] * 100 + sl[1] * 10 + s->vcs[i].pointCount;
+    }
+#pragma omp critical
+    {
+        int k = 0;
+        while (k < 64 && g_topo_w[k] && g_topo_sig[k] != sig) ++k;
+        if (k < 64) { g_topo_sig[k] = sig; g_topo_w[k] += sweeps * (long)s->count; }
+    }
+}
+void b2o_topo_diag(int on, long* sig64, long* w64) {
+    for (int k = 0; k < 64; ++k) { if (sig64) sig64[k] = g_topo_sig[k]; if (w64) w64[k] = g_topo_w[k]; }
+    if (on >= 0) { g_topo_diag = on; for (int k = 0; k < 64; ++k) { g_topo_sig[k] = 0; g_topo_w[k] = 0; } }
+}
+
 static void island_solve(Island* is, World* w, TimeStep step) {
     float h = step.dt;
     for (int i = 0; i < is->bodyCount; ++i) {
@@ -1400,6 +1432,7 @@ static void island_solve(Island* is, World* w, TimeStep step) {
         ++passes;
         if (solver_solve_position(&s, 0, -1, -1)) break;
     }
+    if (g_topo_diag && is->contactCount >= 3 && is->contactCount <= 4) topo_record(&s, is, sweeps);
     if (is->contactCount > 0) {
         int dyn[256], lp = 0, pts = 0, n1 = 0, n2 = 0;
         for (int k = 0; k < is->bodyCount && k < 256; ++k) dyn[k] = is->bodies[k]->invMass > 0.0f || is->bodies[k]->invI > 0.0f;

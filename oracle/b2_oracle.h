@@ -172,6 +172,8 @@ void b2o_set_listener(World* w, ContactCb begin, ContactCb end, void* ctx);
 void b2o_period_diag(int on, long* out300);
 /* diagnostic: the work model counts velocity sweeps as if periods up to p were detected (0 = the device) */
 void b2o_model_period(int p);
+/* diagnostic: topology histogram of 3- and 4-contact islands (see b2_oracle.c) */
+void b2o_topo_diag(int on, long* sig64, long* w64);
 
 /* body API used by the env layer (pybox2d semantics) */
 void b2o_set_linear_velocity(Body* b, V2 v);
