@@ -36,7 +36,7 @@ template <int ENV> struct Env : World<ENV> {
         constexpr int TN = W::LS::TN;
         for (int i = 0; i < TN; ++i) { S.tpar[i] = i + 1 < TN ? i + 1 : NULLN; S.th[i] = -1; S.tud[i] = -1; S.tc1[i] = NULLN; S.tc2[i] = NULLN; }
         S.root = NULLN; S.freeList = 0; S.nodeCount = 0; S.moveCount = 0;
-        S.cHead = NULLN; S.cFree = 0; S.cCount = 0;
+        S.cHead = NULLN; S.cFree = 0; S.cCount = 0; S.cHW = 0;
         for (int c = 0; c < D::CMAX; ++c) S.cnext[c] = c + 1 < D::CMAX ? c + 1 : NULLN;
         S.inv_dt0 = 0.0f; S.newFixture = 0; S.haveBodies = 0; S.episode = 0; S.stepCounter = 0;
         S.elapsed = 0; S.blks_in_place = 0; S.prev_blks_in_place = 0; S.wall_contact = 0;
@@ -353,7 +353,18 @@ template <int ENV> struct Env : World<ENV> {
 
     // reset(): destroy + rebuild from sh.draws, then the reference's step with sh.act
     __device__ __forceinline__ void env_reset_coop() {
+        {   // the contact slots used since the last reset back to their initial contents (destroy_bodies
+            // rebuilds the free chain), so every slot is initial again (LaneState::cHW)
+            using LS = typename W::LS;
+            const int hw = S.cHW;
+            typedef uint32_t __attribute__((__may_alias__)) aw_t;
+            aw_t* w = reinterpret_cast<aw_t*>(S.cprev);   // cprev .. mid[1]: NCA - 1 arrays
+            for (int i = tid; i < (LS::NCA - 1) * D::CMAX; i += 64)   // the wave
+                if (i % D::CMAX < hw) w[i] = 0u;
+        }
+        __syncthreads();
         if (tid == 0) {
+            S.cHW = 0;
             destroy_bodies();
             create_bodies(sh.draws);
             calc_distances();

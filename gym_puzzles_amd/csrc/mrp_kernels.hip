@@ -498,7 +498,8 @@ int mrp_debug_progress(int device, uint32_t** host_words, int n_lanes) {
 }
 
 int mrp_debug_velbench(int device, int nc, int pcount, int iters, int blocks, uint64_t* cycles) {
-    if (nc < 1 || nc > 16 || pcount < 1 || pcount > 2 || blocks < 1 || !cycles || hipSetDevice(device) != hipSuccess) return MRP_E_ARG;
+    const int ncc = nc >= 100 ? nc - 100 : nc;   // nc >= 100: a chain of nc - 100 contacts (k_velbench); ncc + 1 bodies <= v0's 7
+    if (ncc < 1 || ncc > 6 || pcount < 1 || pcount > 2 || blocks < 1 || !cycles || hipSetDevice(device) != hipSuccess) return MRP_E_ARG;
     EnvTables all[N_ENVS];
     for (int i = 0; i < N_ENVS; ++i) build_tables(i, all[i]);
     unsigned long long* d = nullptr;

@@ -52,6 +52,67 @@ __device__ __forceinline__ void store_state(const LaneState<ENV>& S, uint32_t* _
     for (int i = tid; i < NQ; i += BLOCK) dst[i] = w[i];
 }
 
+// words [A, B) of a lane's state, 16-B granules where aligned (A, B compile-time)
+template <int A, int B, bool LOAD>
+__device__ __forceinline__ void move_words(word_t* lds, word_t* g, int tid) {
+    constexpr int QA = (A + 3) / 4, QB = B / 4;
+    typedef uint4 __attribute__((__may_alias__)) quad_t;
+    if (QA < QB) {
+        for (int i = QA + tid; i < QB; i += BLOCK) {
+            if (LOAD) reinterpret_cast<quad_t*>(lds)[i] = reinterpret_cast<const quad_t*>(g)[i];
+            else reinterpret_cast<quad_t*>(g)[i] = reinterpret_cast<const quad_t*>(lds)[i];
+        }
+        constexpr int H = 4 * QA - A, T = B - 4 * QB;   // head / tail words outside the granules
+        if (tid < H + T) {
+            const int k = tid < H ? A + tid : 4 * QB + (tid - H);
+            if (LOAD) lds[k] = g[k]; else g[k] = lds[k];
+        }
+    } else {
+        for (int k = A + tid; k < B; k += BLOCK) { if (LOAD) lds[k] = g[k]; else g[k] = lds[k]; }
+    }
+}
+// k_step's state round trip: everything but the contact slots >= cHW, which hold their initial
+// contents in HBM and are rebuilt in LDS (LaneState::cHW).  `hw` = the slots to move (load: the
+// stored cHW; store: max(cHW at load, cHW now), so slots a reset in this launch zeroed are
+// written back as well).
+template <int ENV>
+struct StateIO {
+    using LS = LaneState<ENV>;
+    static constexpr int C = LS::C;
+    static constexpr int P = (int)(offsetof(LS, cnext) / 4), Q = (int)(offsetof(LS, inv_dt0) / 4), NW = lane_words<ENV>();
+    static constexpr int HWW = (int)(offsetof(LS, cHW) / 4);
+    static_assert(Q - P == LS::NCA * C, "contact arrays cnext .. mid[1] are contiguous");
+    template <bool LOAD>
+    __device__ __forceinline__ static void contacts(word_t* lds, word_t* g, int hw, int tid) {
+        for (int i = tid; i < LS::NCA * C; i += BLOCK) {
+            const int c = i % C;
+            if (c < hw) {
+                if (LOAD) lds[P + i] = g[P + i]; else g[P + i] = lds[P + i];
+            } else if (LOAD) {
+                lds[P + i] = i < C ? (c + 1 < C ? (uint32_t)(c + 1) : (uint32_t)NULLN) : 0u;
+            }
+        }
+    }
+    // hw_io <- the loaded cHW (clamped to the pool; kept in LDS, not live in registers across the step)
+    __device__ __forceinline__ static void load(LS& S, int& hw_io, const uint32_t* __restrict__ gs, int lane, int tid) {
+        word_t* g = const_cast<uint32_t*>(gs) + (size_t)lane * NW;
+        word_t* lds = reinterpret_cast<word_t*>(&S);
+        const int hw = min(max((int)__builtin_amdgcn_readfirstlane(g[HWW]), 0), C);
+        move_words<0, P, true>(lds, g, tid);
+        move_words<Q, NW, true>(lds, g, tid);
+        contacts<true>(lds, g, hw, tid);
+        if (tid == 0) hw_io = hw;
+    }
+    __device__ __forceinline__ static void store(const LS& S, const int& hw_io, uint32_t* __restrict__ gs, int lane, int tid) {
+        word_t* g = gs + (size_t)lane * NW;
+        word_t* lds = const_cast<word_t*>(reinterpret_cast<const word_t*>(&S));
+        const int hw = max(hw_io, min(max(S.cHW, 0), C));
+        move_words<0, P, false>(lds, g, tid);
+        move_words<Q, NW, false>(lds, g, tid);
+        contacts<false>(lds, g, hw, tid);
+    }
+};
+
 // copy this env's hot tables from __constant__ memory into the lane's LDS (before the
 // barrier that follows load_state)
 template <int ENV>
@@ -130,7 +191,11 @@ __global__ __launch_bounds__(BLOCK, 4) void k_reset(uint32_t* state, int nl, con
 
 template <int ENV, bool MULTI>
 #ifndef MRP_STEP_WAVES_PER_EU
-#define MRP_STEP_WAVES_PER_EU 4   // 4 waves per SIMD: all 4096 lanes of a GPU resident at once (LDS allows 16 per CU)
+// 3 waves per SIMD (168 VGPRs): k_step without VGPR spills in the solver phases.  At 4 (128 VGPRs,
+// all 4096 lanes of a GPU resident at once) the kernel carried 54 VGPR spills whose scratch traffic
+// was 12.7 MB of its 46.7 MB per v0 launch; the driver window runs at the same rate either way
+// (profiles/r3c_ab_occ3_regs3.txt, profiles/r3c_ab_occ3_trim.txt, profiles/r3c_traffic_occ3_trim.txt)
+#define MRP_STEP_WAVES_PER_EU 3
 #endif
 __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t* state, int nl, const float* actions, float* obs, float* reward,
                                                 double* reward64, uint8_t* done_out, uint8_t* trunc_out, uint8_t* status_out, float* term_obs,
@@ -153,7 +218,7 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t*
     if (tid < MRP_TRACE_W) sh.trace[tid] = 0;
     long long toi0 = 0, pos0 = 0;
 #endif
-    load_state<ENV>(sh.S, state, lane, tid);
+    StateIO<ENV>::load(sh.S, sh.hw_io, state, lane, tid);
     load_tables<ENV>(sh.lt, tid);
     __syncthreads();
 #ifdef MRP_STAMPS
@@ -215,7 +280,7 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t*
         for (int k = tid; k < D::OBS; k += BLOCK) obs[row * D::OBS + k] = sh.obs[k];
         __syncthreads();
     }
-    store_state<ENV>(sh.S, state, lane, tid);
+    StateIO<ENV>::store(sh.S, sh.hw_io, state, lane, tid);
     if (cost && tid == 0) cost[lane] = (uint32_t)min(__builtin_amdgcn_s_memtime() - t_start, 0xffffffffull);
     MRP_STAMP(10);
 #ifdef MRP_STAMPS
@@ -369,13 +434,17 @@ namespace {
 // Diagnostic micro-benchmark of the lane-distributed velocity sweeps (mrp_debug_velbench): a
 // synthetic v0 island of nc agent-block contacts with pcount manifold points each, swept `iters`
 // times with the early exit off; out[block] = s_memtime cycles of the sweeps.
-__global__ __launch_bounds__(BLOCK, 4) void k_velbench(int nc, int pcount, int iters, unsigned long long* out) {
+__global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_velbench(int nc, int pcount, int iters, unsigned long long* out) {
     using W = World<0>;
     __shared__ Shared<0> sh;
     const int tid = threadIdx.x;
     EnvParams P{};
     W w(sh, g_tables[0], P, tid);
     auto& is = sh.isl;
+    // nc >= 100: a chain of nc - 100 contacts (contact i between bodies i and i + 1, all moving):
+    // serial within a sweep, pipelined across sweeps by solver_velocity_pipe
+    const bool chain = nc >= 100;
+    if (chain) nc -= 100;
     if (tid == 0) {
         is.nb = nc + 1; is.nc = nc;
         for (int b = 0; b <= nc; ++b) { is.vvx[b] = 0.3f * b - 0.1f; is.vvy[b] = 0.2f - 0.05f * b; is.vw[b] = b == 0 ? 0.01f : 0.0f; }
@@ -385,6 +454,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_velbench(int nc, int pcount, int i
             vc.nx = __cosf(ang); vc.ny = __sinf(ang);
             vc.iaI = i + 1; vc.ibI = 0; vc.mA = 1.0f; vc.iA = 0.0f; vc.mB = 0.05f; vc.iB = 1.0f / 17.0833f; vc.friction = 0.44f;
             vc.pointCount = pcount;
+            if (chain) { vc.iaI = i; vc.ibI = i + 1; vc.mA = 1.0f; vc.iA = 0.05f; }
             for (int j = 0; j < 2; ++j) {
                 vc.rAx[j] = 0.1f * j - 0.2f; vc.rAy[j] = 0.75f; vc.rBx[j] = 0.4f + 0.3f * j; vc.rBy[j] = -0.6f;
                 vc.ni[j] = 0.2f; vc.ti[j] = 0.01f; vc.vbias[j] = 0.0f; vc.nmass[j] = 0.9f; vc.tmass[j] = 0.8f;
@@ -396,7 +466,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_velbench(int nc, int pcount, int i
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     int sw = nc == 1 ? w.solver_velocity_one(is, sh.u.sol.vcs, iters, false)
                      : (nc == 2 ? w.solver_velocity_two(is, sh.u.sol.vcs, iters, false) : -1);
-    if (sw < 0) w.solver_velocity_lanes(is, sh.u.sol.vcs, iters, false);
+    if (sw < 0) { if (MRP_PIPE) w.solver_velocity_pipe(is, sh.u.sol.vcs, iters, false); else w.solver_velocity_lanes(is, sh.u.sol.vcs, iters, false); }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     __syncthreads();
     if (tid == 0) out[blockIdx.x] = t1 - t0 + (is.vvx[0] == 12345.0f ? 1ull : 0ull);

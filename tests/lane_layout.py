@@ -27,7 +27,7 @@ def fields(env_id: int):
     for n in ("root", "freeList", "nodeCount", "moveCount"):
         f.append((n, 1))
     f.append(("moveBuf", MOVE_N))
-    for n in ("cHead", "cFree", "cCount", "pad0"):
+    for n in ("cHead", "cFree", "cCount", "cHW"):
         f.append((n, 1))
     for n in ("cnext", "cprev", "cfa", "cfb", "cflags", "ctoiCount", "ctoi", "cfric", "mpc", "mtype",
               "mlnx", "mlny", "mlpx", "mlpy"):
