@@ -441,8 +441,7 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_velbench(int n
     EnvParams P{};
     W w(sh, g_tables[0], P, tid);
     auto& is = sh.isl;
-    // nc >= 100: a chain of nc - 100 contacts (contact i between bodies i and i + 1, all moving):
-    // serial within a sweep, pipelined across sweeps by solver_velocity_pipe
+    // nc >= 100: a chain of nc - 100 contacts (contact i between bodies i and i + 1, all moving)
     const bool chain = nc >= 100;
     if (chain) nc -= 100;
     if (tid == 0) {
@@ -466,7 +465,7 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_velbench(int n
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     int sw = nc == 1 ? w.solver_velocity_one(is, sh.u.sol.vcs, iters, false)
                      : (nc == 2 ? w.solver_velocity_two(is, sh.u.sol.vcs, iters, false) : -1);
-    if (sw < 0) { if (MRP_PIPE) w.solver_velocity_pipe(is, sh.u.sol.vcs, iters, false); else w.solver_velocity_lanes(is, sh.u.sol.vcs, iters, false); }
+    if (sw < 0) w.solver_velocity_lanes(is, sh.u.sol.vcs, iters, false);
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     __syncthreads();
     if (tid == 0) out[blockIdx.x] = t1 - t0 + (is.vvx[0] == 12345.0f ? 1ull : 0ull);

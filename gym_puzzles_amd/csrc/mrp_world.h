@@ -79,10 +79,6 @@ constexpr int MRP_FAULT_TREE_UP = 1, MRP_FAULT_TREE_DOWN = 2, MRP_FAULT_TREE_REM
 // oracle's high-water marks against them); a full pool records its code and the insertion is
 // skipped, so no index ever leaves its array.
 constexpr int MRP_FAULT_TREE_POOL = 9, MRP_FAULT_CONTACT_POOL = 10, MRP_FAULT_MOVE_BUFFER = 11, MRP_FAULT_ISLAND_POOL = 12;
-constexpr int MRP_FAULT_PIPE = 13;
-#ifndef MRP_PIPE
-#define MRP_PIPE 0   // islands of 3+ contacts: 1 = pipelined sweeps (solver_velocity_pipe), 0 = contact by contact (solver_velocity_lanes)
-#endif   // solver_velocity_pipe made no progress (never in a valid solve)
 constexpr float LINEAR_SLOP = 0.005f;
 constexpr float AABB_EXT = 0.1f;
 constexpr float AABB_MUL = 2.0f;
@@ -206,7 +202,6 @@ template <int ENV> struct Shared {
     IslT<NBODY, C> isl;
     int stack[NBODY];
     int isl_go;
-    uint8_t ptl[NBODY * C];   // solver_velocity_pipe: island body k's contacts in order, 2 * contact + side
     int hw_io;   // LaneState::cHW as k_step loaded it (its store writes slots < max(hw_io, cHW) back)
     float salpha0[4];
     // collide: contact list snapshot (the per-contact manifolds live in the phase union below)
@@ -1081,124 +1076,6 @@ template <int ENV> struct World {
         return sweeps;
     }
 
-    // ---------------------------------------------------------------- pipelined velocity sweeps
-    // b2ContactSolver::SolveVelocityConstraints x `iters` for islands of 3..64 contacts, with the
-    // sweeps unrolled into their dependency DAG: contact i's update of sweep s may run as soon as
-    // every dynamic body it touches has received exactly the updates that precede it in the
-    // reference's order (sweep by sweep, contact by contact).  Each body's sequence of updates,
-    // and each contact's, is then the serial one, so every float operation sees the operands of
-    // the serial Gauss-Seidel and the result is bitwise the same; updates on disjoint dynamic
-    // bodies (also from different sweeps) run in the same round.  Static bodies (walls) keep their
-    // +0 velocity through every update (+0 + 0 * P = +0), so they order nothing.
-    // Lanes: contact i's constants and impulses in lane i, island body k's velocity in lane k
-    // together with its progress (bt sweeps complete + bp updates into the current one).  One
-    // round: contacts fetch their bodies (ds_bpermute) and test readiness, the ready ones update
-    // (per-lane block-solver cases), and each dynamic body pulls the result of the contact that is
-    // next in its order (sh.ptl) if that contact was ready.
-    // Exact early exit as solver_velocity_lanes: every lane records its own state after sweeps
-    // t = iters - 2 (mod 4) (snapshot) and t = iters (mod 4) (compare + keep); the check of sweep T
-    // resolves once every lane has completed T, and no contact may complete sweep T + 4 before
-    // that, so the kept state of sweep T is still there to be restored when the check succeeds.
-    __device__ __forceinline__ static float bperm(float v, int src) { return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v))); }
-    __device__ __forceinline__ static int bpermi(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
-    __device__ __forceinline__ static bool same_bits(P2 a, P2 b) {
-        return __float_as_uint(a.x) == __float_as_uint(b.x) && __float_as_uint(a.y) == __float_as_uint(b.y);
-    }
-    __device__ __forceinline__ int solver_velocity_pipe(Isl& is, VC* vcs, int iters, bool early_exit = true) {
-        const int nc = __builtin_amdgcn_readfirstlane(is.nc), nb = __builtin_amdgcn_readfirstlane(is.nb);
-        const bool isc = tid < nc, isb = tid < nb;
-        const int ci = isc ? tid : 0;
-        CC my = load_cc(vcs[ci]);
-        const int ca = vcs[ci].iaI, cb = vcs[ci].ibI;
-        const bool dA = isc && (vcs[ci].mA != 0.0f || vcs[ci].iA != 0.0f);
-        const bool dB = isc && (vcs[ci].mB != 0.0f || vcs[ci].iB != 0.0f);
-        const uint64_t mdA = __builtin_amdgcn_ballot_w64(dA), mdB = __builtin_amdgcn_ballot_w64(dB);
-        // contact lane: its rank among the contacts touching each of its bodies (the reference's
-        // order); body lane: how many contacts touch it, and whether it moves
-        int rA = 0, rB = 0, deg = 0;
-        bool dk = false;
-        for (int j = 0; j < nc; ++j) {
-            const int ja = rdli(ca, j), jb = rdli(cb, j);
-            if (j < tid) { rA += (ja == ca) | (jb == ca); rB += (ja == cb) | (jb == cb); }
-            if (ja == tid) { deg += 1; dk |= ((mdA >> j) & 1ull) != 0; }
-            if (jb == tid) { deg += 1; dk |= ((mdB >> j) & 1ull) != 0; }
-        }
-        dk = dk && isb;
-        if (dA) sh.ptl[ca * C + rA] = (uint8_t)(2 * tid);
-        if (dB) sh.ptl[cb * C + rB] = (uint8_t)(2 * tid + 1);
-        __syncthreads();
-        const int bk = isb ? tid : 0;
-        float bvx = is.vvx[bk], bvy = is.vvy[bk], bw = is.vw[bk];
-        int bt = 0, bp = 0;   // body lane: sweeps complete, updates into the next one
-        int s = 0;            // contact lane: updates done (= sweeps complete)
-        // kept states: snapshot (sweep iters - 2 mod 4), current (sweep iters mod 4), per lane
-        P2 sni = my.ni, sti = my.ti, cni = my.ni, cti = my.ti;
-        float sbx = bvx, sby = bvy, sbw = bw, cbx = bvx, cby = bvy, cbw = bw;
-        bool difc = false, difb = false;
-        // first check: the smallest T >= 2 with iters - T = 0 (mod 4) (its snapshot, T - 2, may be
-        // the initial state: snap_initial)
-        int Tp = iters & 3;
-        if (Tp < 2) Tp += 4;
-        if (!early_exit) Tp = iters + 4;
-        int sweeps = iters;
-        for (int round = 0;; ++round) {
-            if (round > 64 * iters + 64) { if (tid == 0) S.fault = MRP_FAULT_PIPE; break; }   // never in a valid solve
-            const int code = bt * 64 + bp;
-            const float ax = bperm(bvx, ca), ay = bperm(bvy, ca), aw = bperm(bw, ca);
-            const float bx = bperm(bvx, cb), by = bperm(bvy, cb), bwv = bperm(bw, cb);
-            const int acode = bpermi(code, ca), bcode = bpermi(code, cb);
-            const int e = dk ? (int)sh.ptl[tid * C + bp] : 0;
-            const bool ready = isc && s < iters && s <= Tp + 2 && (!dA || acode == s * 64 + rA) && (!dB || bcode == s * 64 + rB);
-            P2 vA = p2(ax, ay), vB = p2(bx, by);
-            float wA = aw, wB = bwv;
-            if (ready) {
-                P2 ni, ti;
-                vel_update(my, my.pcount, [](bool x) { return x; }, ni, ti, vA, wA, vB, wB);
-                my.ni = ni; my.ti = ti;
-                ++s;
-                const int left = iters - s;
-                if ((left & 3) == 2) { sni = my.ni; sti = my.ti; }
-                else if ((left & 3) == 0 && s >= 2) {
-                    difc = !(same_bits(my.ni, sni) && same_bits(my.ti, sti));
-                    cni = my.ni; cti = my.ti;
-                }
-            }
-            // each moving body takes the result of the contact next in its order, if that one ran
-            const int src = e >> 1;
-            const float pax = bperm(vA.x, src), pay = bperm(vA.y, src), paw = bperm(wA, src);
-            const float pbx = bperm(vB.x, src), pby = bperm(vB.y, src), pbw = bperm(wB, src);
-            const int prdy = bpermi(ready ? 1 : 0, src);
-            if (dk && prdy) {
-                const bool side = e & 1;
-                bvx = side ? pbx : pax; bvy = side ? pby : pay; bw = side ? pbw : paw;
-                if (++bp == deg) {
-                    bp = 0; ++bt;
-                    const int left = iters - bt;
-                    if ((left & 3) == 2) { sbx = bvx; sby = bvy; sbw = bw; }
-                    else if ((left & 3) == 0 && bt >= 2) {
-                        difb = __float_as_uint(bvx) != __float_as_uint(sbx) || __float_as_uint(bvy) != __float_as_uint(sby) ||
-                               __float_as_uint(bw) != __float_as_uint(sbw);
-                        cbx = bvx; cby = bvy; cbw = bw;
-                    }
-                }
-            }
-            if (Tp <= iters && __builtin_amdgcn_ballot_w64((isc && s < Tp) || (dk && bt < Tp)) == 0) {
-                // every lane has completed sweep Tp: the state after Tp vs the state after Tp - 2
-                if (__builtin_amdgcn_ballot_w64(difc || difb) == 0) {
-                    sweeps = Tp;
-                    my.ni = cni; my.ti = cti;
-                    if (dk) { bvx = cbx; bvy = cby; bw = cbw; }
-                    break;
-                }
-                Tp += 4;
-            }
-            if (__builtin_amdgcn_ballot_w64((isc && s < iters) || (dk && bt < iters)) == 0) break;
-        }
-        if (isb) { is.vvx[tid] = bvx; is.vvy[tid] = bvy; is.vw[tid] = bw; }
-        if (isc) store_cc(vcs[tid], my);
-        return sweeps;
-    }
-
     // Register-resident sweeps for islands of one or two contacts (nine in ten islands of a v0
     // rollout have one, most of the rest two): every lane runs the same contact updates on the
     // same values, so the bodies' velocities and the impulses stay in registers through all the
@@ -1826,7 +1703,7 @@ template <int ENV> struct World {
             if (nc > 0 && nc <= 64) {
                 set_prio(lvl > step_prio ? lvl : step_prio);
                 int sweeps = nc == 1 ? solver_velocity_one(is, sh.u.sol.vcs, 180) : (nc == 2 ? solver_velocity_two(is, sh.u.sol.vcs, 180) : -1);
-                if (sweeps < 0) sweeps = MRP_PIPE ? solver_velocity_pipe(is, sh.u.sol.vcs, 180) : solver_velocity_lanes(is, sh.u.sol.vcs, 180);
+                if (sweeps < 0) sweeps = solver_velocity_lanes(is, sh.u.sol.vcs, 180);
                 MRP_TRACE(15, sweeps * nc);
                 (void)sweeps;
             }
@@ -2291,7 +2168,7 @@ template <int ENV> struct World {
                 if (nc <= 64) {
                     int sweeps = nc == 1 ? solver_velocity_one(sh.isl, sh.u.sol.vcs, 180)
                                          : (nc == 2 ? solver_velocity_two(sh.isl, sh.u.sol.vcs, 180) : -1);
-                    if (sweeps < 0) { if (MRP_PIPE) solver_velocity_pipe(sh.isl, sh.u.sol.vcs, 180); else solver_velocity_lanes(sh.isl, sh.u.sol.vcs, 180); }
+                    if (sweeps < 0) solver_velocity_lanes(sh.isl, sh.u.sol.vcs, 180);
                     set_prio(step_prio);
                 }
                 else if (tid == 0) for (int i = 0; i < 180; ++i) solver_velocity(sh.isl, sh.u.sol.vcs);

@@ -148,8 +148,7 @@ int mrp_get_flags(mrp_ctx* ctx, int32_t* out);
 /* per lane: 0, or the code of the loop guard that ended a runaway loop in that lane (a bound no
  * valid world reaches: tree walks, contact-list walks, islands, TOI passes; see mrp_world.h
  * MRP_FAULT_*: 1-8 loop guards -- tree walks, contact-list walks, islands, TOI passes, pair decoding,
- * island DFS; 9-12 pool guards -- tree nodes, contact slots, move buffer, island arrays; 13 the
- * pipelined velocity sweeps made no progress).  Sticky.
+ * island DFS; 9-12 pool guards -- tree nodes, contact slots, move buffer, island arrays).  Sticky.
  * int32 [n_lanes] */
 int mrp_get_faults(mrp_ctx* ctx, int32_t* out);
 /* summed over lanes: TOI events and position-solver iterations (diagnostics) */
