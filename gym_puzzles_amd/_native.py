@@ -11,6 +11,8 @@ import os
 
 import numpy as np
 
+from .spawn import ENV_VERSION
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmrp.so")
 
@@ -28,7 +30,12 @@ ENV_IDS = {
     "MultiRobotPuzzleHeavy-v2-3block": 4,
     "MultiRobotPuzzle-v3": 5,
     "MultiRobotPuzzle-v3-heavy": 6,      # RobotPuzzleBase(heavy=True) (tests/test_env.py:12)
+    # MultiRobotPuzzle2 / MultiRobotPuzzleHeavy2(num_agents=N) (multi_robot_puzzle_02.py:139)
+    "MultiRobotPuzzle-v2-agents1": 7, "MultiRobotPuzzle-v2-agents3": 8, "MultiRobotPuzzle-v2-agents4": 9,
+    "MultiRobotPuzzle-v2-agents5": 10, "MultiRobotPuzzleHeavy-v2-agents1": 11, "MultiRobotPuzzleHeavy-v2-agents3": 12,
+    "MultiRobotPuzzleHeavy-v2-agents4": 13, "MultiRobotPuzzleHeavy-v2-agents5": 14,
 }
+MAXF = 24   # csrc/mrp_config.h: fixtures per env (mrp_shapes fills MAXF rows)
 
 # every symbol include/mrp.h declares (tests/test_abi.py checks the .so exports all of them)
 EXPORTED = (
@@ -136,8 +143,8 @@ def shapes(env_id: int) -> dict:
     """Fixture geometry of an env (host-only; creation order, local vertices)."""
     L = load()
     n = ctypes.c_int32()
-    fb, cnt = np.zeros(16, np.int32), np.zeros(16, np.int32)
-    v = np.zeros((16, 8, 2), np.float32)
+    fb, cnt = np.zeros(MAXF, np.int32), np.zeros(MAXF, np.int32)
+    v = np.zeros((MAXF, 8, 2), np.float32)
     if L.mrp_shapes(env_id, ctypes.byref(n), _p(fb), _p(cnt), _p(v)) != MRP_OK:
         raise ValueError(f"unknown env_id {env_id}")
     return {"n_fix": n.value, "fix_body": fb[:n.value], "counts": cnt[:n.value], "verts": v[:n.value]}
@@ -188,9 +195,9 @@ class Batch:
 
     def set_reward_params(self, agentDelta=None, agentDistance=None, blockDelta=None, blockDistance=None,
                           puzzleComp=None, outOfBounds=1000, blkOutOfBounds=100):
-        v0 = self.env_id < 2 or self.env_id >= 5   # v3 defaults equal v0's (core.py:149-155)
+        v0 = ENV_VERSION[self.env_id] != 2   # v3 defaults equal v0's (core.py:149-155)
         if puzzleComp is None:
-            puzzleComp = 100 if self.env_id >= 5 else 10000
+            puzzleComp = 100 if ENV_VERSION[self.env_id] == 3 else 10000
         agentDelta = 10 if agentDelta is None else agentDelta
         agentDistance = (0.1 if v0 else 0.25) if agentDistance is None else agentDistance
         blockDelta = (50 if v0 else 25) if blockDelta is None else blockDelta
@@ -301,7 +308,7 @@ class Batch:
     def render(self, lanes=None, width: int | None = None, height: int | None = None) -> np.ndarray:
         """rgb_array frames of the selected lanes: uint8 [n, height, width, 3] (row 0 = top),
         the reference's render(mode='rgb_array') (multi_robot_puzzle_00.py:528-592)."""
-        w0, h0 = (1440, 810) if 2 <= self.env_id <= 4 else (640, 480)   # v0 and v3: 640 x 480
+        w0, h0 = (1440, 810) if ENV_VERSION[self.env_id] == 2 else (640, 480)   # v0 and v3: 640 x 480
         width, height = width or w0, height or h0
         sel = np.ascontiguousarray(np.arange(self.n_lanes) if lanes is None else np.atleast_1d(lanes), np.int32)
         out = np.zeros((len(sel), height, width, 3), np.uint8)

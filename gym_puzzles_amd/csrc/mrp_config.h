@@ -4,7 +4,9 @@
 // Env ids follow include/mrp.h: 0 MultiRobotPuzzle-v0, 1 MultiRobotPuzzleHeavy-v0,
 // 2 MultiRobotPuzzle-v2, 3 MultiRobotPuzzleHeavy-v2, 4 Heavy-v2 with the build-defined
 // 3-block square, 5 MultiRobotPuzzle-v3 (RobotPuzzleBase,
-// core.py), 6 v3 constructed with heavy=True (tests/test_env.py:12).
+// core.py), 6 v3 constructed with heavy=True (tests/test_env.py:12), 7-10 MultiRobotPuzzle2
+// constructed with num_agents = 1, 3, 4, 5 and 11-14 MultiRobotPuzzleHeavy2 with the same
+// agent counts (multi_robot_puzzle_02.py:139,151,354).
 #pragma once
 #include "mrp_math.h"
 
@@ -14,11 +16,8 @@ namespace mrp {
 constexpr int MRP_STATUS_NONFINITE_BIT = 0x40, MRP_STATUS_FAULT_BIT = 0x80;
 
 constexpr int MAX_POLY = 8;
-constexpr int TREE_N = 32;    // largest dynamic-tree node pool (15 proxies in the 3-block config)
-constexpr int MOVE_N = 16;    // move buffer: at most NF (<= 15) proxies move between two UpdatePairs
-constexpr int MAXB = 9;       // bodies: <= 3 blocks + 5 agents ... + 4 walls (max over configs: 1 + 5 + 4 = 10)
-constexpr int MAXBODY = 10;
-constexpr int MAXF = 16;
+constexpr int MAXBODY = 10;   // bodies: blocks + agents + 4 walls (max over configs: 1 + 5 + 4)
+constexpr int MAXF = 24;      // fixtures (max over configs: v2 with 5 agents, 2 + 5 * 3 + 4 = 21)
 constexpr int MAXV = 16;
 constexpr int MAXDRAW = 16;
 
@@ -32,12 +31,45 @@ template <> struct Dims<3> { static constexpr int V = 2, NA = 2, NB = 1, NF = 12
 template <> struct Dims<4> { static constexpr int V = 2, NA = 2, NB = 3, NF = 15, CMAX = 91, OBS = 69, ACT = 4, NDRAW = 9; };
 template <> struct Dims<5> { static constexpr int V = 3, NA = 2, NB = 1, NF = 8, CMAX = 21, OBS = 27, ACT = 6, NDRAW = 7; };
 template <> struct Dims<6> { static constexpr int V = 3, NA = 2, NB = 1, NF = 8, CMAX = 21, OBS = 27, ACT = 6, NDRAW = 7; };
-constexpr int N_ENVS = 7;
+// MultiRobotPuzzle2(num_agents = N) (multi_robot_puzzle_02.py:139): one T block (2 fixtures),
+// N agents (body + 2 wheels), 4 walls; CMAX = fixture pairs on different bodies, not both static
+template <int N> struct DimsV2 {
+    static constexpr int DF = 2 + 3 * N;   // dynamic fixtures
+    static constexpr int V = 2, NA = N, NB = 1, NF = DF + 4, CMAX = DF * (DF - 1) / 2 - 1 - 3 * N + 4 * DF,
+                         OBS = 9 * N + 4 + 16 + 1, ACT = 2 * N, NDRAW = 1 + 2 * N + 2;
+};
+template <> struct Dims<7> : DimsV2<1> {};
+template <> struct Dims<8> : DimsV2<3> {};
+template <> struct Dims<9> : DimsV2<4> {};
+template <> struct Dims<10> : DimsV2<5> {};
+template <> struct Dims<11> : DimsV2<1> {};
+template <> struct Dims<12> : DimsV2<3> {};
+template <> struct Dims<13> : DimsV2<4> {};
+template <> struct Dims<14> : DimsV2<5> {};
+static_assert(DimsV2<2>::CMAX == Dims<2>::CMAX && DimsV2<2>::OBS == Dims<2>::OBS && DimsV2<2>::NF == Dims<2>::NF &&
+              DimsV2<2>::NDRAW == Dims<2>::NDRAW, "DimsV2 restates the registered v2 layout");
+constexpr int N_ENVS = 15;
+
+// Per env id: version (0 v0, 2 v2, 3 v3), agents, blocks, heavy block, registered TimeLimit.
+struct EnvCfg { int version, n_agents, n_blocks, heavy, max_steps; };
+constexpr EnvCfg ENV_CFG[N_ENVS] = {
+    {0, 2, 1, 0, 2000}, {0, 5, 1, 1, 3000}, {2, 2, 1, 0, 2000}, {2, 2, 1, 1, 2000}, {2, 2, 3, 1, 2000},
+    {3, 2, 1, 0, 1500}, {3, 2, 1, 1, 1500},
+    {2, 1, 1, 0, 2000}, {2, 3, 1, 0, 2000}, {2, 4, 1, 0, 2000}, {2, 5, 1, 0, 2000},
+    {2, 1, 1, 1, 2000}, {2, 3, 1, 1, 2000}, {2, 4, 1, 1, 2000}, {2, 5, 1, 1, 2000},
+};
 
 // Node pool of a lane's dynamic tree.  b2DynamicTree starts at 16 nodes and doubles only when
 // all are live; a world holds at most 2 * proxies - 1 live nodes, so an env with <= 8 proxies
-// never grows past 16 and its node ids (free-list order) never exceed 15.
-template <int ENV> constexpr int tree_n() { return 2 * Dims<ENV>::NF - 1 <= 16 ? 16 : 32; }
+// never grows past 16 and its node ids (free-list order) never exceed 15.  A pool allocated at
+// its final size with the free list in index order hands out the same ids as Box2D's doubling
+// pool (the doubled part is appended to the free list in index order once the old part is full).
+template <int ENV> constexpr int tree_n() {
+    return 2 * Dims<ENV>::NF - 1 <= 16 ? 16 : (2 * Dims<ENV>::NF - 1 <= 32 ? 32 : 64);
+}
+// Move buffer: at most NF proxies are buffered between two UpdatePairs (every proxy after a
+// reset's CreateProxy calls; a moved proxy at most once per Solve / TOI sub-step)
+template <int ENV> constexpr int move_n() { return Dims<ENV>::NF < 16 ? 16 : 32; }
 
 struct ShapeDef {
     int count;

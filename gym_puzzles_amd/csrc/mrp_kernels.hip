@@ -122,11 +122,19 @@ static int words_for(int env_id) {
     return o ? o->words : -1;
 }
 
+// the host tables and the env's compile-time layout (Dims<ENV> of its unit) describe the same world
+static bool layout_matches(int env_id, const EnvTables& t) {
+    const EnvOps* o = env_ops(env_id);
+    return o && o->dims[0] == t.obs_dim && o->dims[1] == t.act_dim && o->dims[2] == t.n_draws && o->dims[3] == t.n_agents &&
+           o->dims[4] == t.n_blocks && o->dims[5] == t.n_fix;
+}
+
 extern "C" {
 
 int mrp_env_dims(int env_id, int* obs_dim, int* act_dim, int* n_draws, int* n_agents, int* n_blocks, int* max_steps) {
     EnvTables t;
     if (!build_tables(env_id, t)) return MRP_E_ARG;
+    if (!layout_matches(env_id, t)) return MRP_E_STATE;
     if (obs_dim) *obs_dim = t.obs_dim;
     if (act_dim) *act_dim = t.act_dim;
     if (n_draws) *n_draws = t.n_draws;
@@ -163,6 +171,10 @@ int mrp_create(int env_id, int n_lanes, int device, uint64_t seed, uint64_t lane
     *out = nullptr;
     EnvTables tables;
     if (!build_tables(env_id, tables)) { g_create_error = "bad env_id"; return MRP_E_ARG; }
+    if (!layout_matches(env_id, tables)) {
+        g_create_error = "env tables disagree with the compiled layout of env_id " + std::to_string(env_id);
+        return MRP_E_STATE;
+    }
     if (n_lanes <= 0) { g_create_error = "n_lanes must be > 0"; return MRP_E_ARG; }
     // the velocity solver drops the (then identically +0) restitution velocity bias (mrp_world.h CC):
     // every fixture of every env has the default restitution 0 (no reference fixtureDef sets one)
@@ -268,7 +280,7 @@ int mrp_update_params(mrp_ctx* ctx, double timestep, double decay) {
 
 int mrp_update_goal(mrp_ctx* ctx, double epoch, double nb_epochs) {
     if (!ctx) return MRP_E_ARG;
-    double eps = (ctx->env_id < 2 || ctx->env_id >= 5) ? 25.0 : 0.1;   // v3 stores it too (core.py:161-162), unused
+    double eps = ENV_CFG[ctx->env_id].version != 2 ? 25.0 : 0.1;   // v3 stores it too (core.py:161-162), unused
     ctx->params.scaled_epsilon = eps * (2 - epoch / nb_epochs);
     return MRP_OK;
 }
@@ -558,7 +570,7 @@ int mrp_debug_trace(int device, uint32_t* out, int n_lanes) {
 // ------------------------------------------------------------------------------ rendering
 static int render_args(mrp_ctx* ctx, int W, int H, mrpr::RenderArgs& A) {
     if (W <= 0 || H <= 0 || (int64_t)W * H > (1 << 24)) return MRP_E_ARG;
-    const bool v0 = ctx->env_id <= 1 || ctx->env_id >= 5;   // v0 and v3 share the 640x480 px / SCALE 30 viewport
+    const bool v0 = ENV_CFG[ctx->env_id].version != 2;   // v0 and v3 share the 640x480 px / SCALE 30 viewport
     const double ww = v0 ? 640.0 / 30.0 : 1440.0 / 560.0, wh = v0 ? 480.0 / 30.0 : 810.0 / 560.0;
     A.sx = (float)(ww / W); A.sy = (float)(wh / H);
     A.lw_unit = v0 ? (float)(1.0 / 30.0) : (float)(1.0 / 560.0);

@@ -24,8 +24,8 @@
 
 using namespace mrp;
 
-// this unit's copy of the env tables (uploaded by EnvOps::upload_tables at mrp_create)
-static __constant__ EnvTables g_tables[N_ENVS];
+// this unit's copy of its env's tables (uploaded by EnvOps::upload_tables at mrp_create)
+static __constant__ EnvTables g_table;
 
 #include "mrp_render.h"
 
@@ -118,7 +118,7 @@ struct StateIO {
 template <int ENV>
 __device__ __forceinline__ void load_tables(LdsTables<ENV>& L, int tid) {
     using LT = LdsTables<ENV>;
-    const EnvTables& T = g_tables[ENV];
+    const EnvTables& T = g_table;
     constexpr int SW = LT::NF * (int)(sizeof(ShapeDef) / 4);
     const word_t* src = reinterpret_cast<const word_t*>(T.shape);
     word_t* dst = reinterpret_cast<word_t*>(L.shape);
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(BLOCK) void k_init(uint32_t* state, int nl) {
     if (tid == 0) {
         EnvParams P;
         memset(&P, 0, sizeof(P));
-        Env<ENV> e(sh, g_tables[ENV], P, 0);
+        Env<ENV> e(sh, g_table, P, 0);
         e.init_empty_world();
     }
     __syncthreads();
@@ -158,7 +158,7 @@ template <int ENV>
 __device__ void stage_reset_inputs(Shared<ENV>& sh, const double* draws, const float* actions, int lane, int tid,
                                    uint64_t seed, uint64_t glane) {
     using D = Dims<ENV>;
-    const EnvTables& T = g_tables[ENV];
+    const EnvTables& T = g_table;
     const uint64_t ctr = (uint64_t)(uint32_t)sh.S.episode * 64u;
     if (tid < D::NDRAW)
         sh.draws[tid] = draws ? draws[(size_t)lane * D::NDRAW + tid]
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_reset(uint32_t* state, int nl, con
     load_tables<ENV>(sh.lt, tid);
     __syncthreads();
     stage_reset_inputs<ENV>(sh, draws, actions, lane, tid, seed, lane_offset + lane);
-    Env<ENV> e(sh, g_tables[ENV], P, tid);
+    Env<ENV> e(sh, g_table, P, tid);
     e.env_reset_coop();
     for (int k = tid; k < D::OBS; k += BLOCK) obs[(size_t)lane * D::OBS + k] = sh.obs[k];
     store_state<ENV>(sh.S, state, lane, tid);
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t*
     toi0 = sh.S.toiEvents; pos0 = sh.S.posIters;
 #endif
     MRP_STAMP(0);
-    Env<ENV> e(sh, g_tables[ENV], P, tid);
+    Env<ENV> e(sh, g_table, P, tid);
     if (costmax) {   // priority from the lane's previous-step cost relative to the slowest lane's
         const uint64_t c = cost[lane], m = *costmax;
         e.prio_floor = __builtin_amdgcn_readfirstlane(4 * c > 3 * m ? 3 : (2 * c > m ? 2 : (4 * c > m ? 1 : 0)));
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256) void k_counters(const uint32_t* state, int nl,
 template <int ENV>
 struct Launch {
     static hipError_t upload_tables(const EnvTables* all) {
-        return hipMemcpyToSymbol(HIP_SYMBOL(g_tables), all, sizeof(EnvTables) * N_ENVS);
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_table), all + ENV, sizeof(EnvTables));
     }
     static void init(hipStream_t s, uint32_t* state, int nl) {
         hipLaunchKernelGGL(k_init<ENV>, dim3(nl), dim3(BLOCK), 0, s, state, nl);
@@ -413,7 +413,9 @@ struct Launch {
 #endif
     }
     static constexpr EnvOps ops() {
-        return EnvOps{lane_words<ENV>(), (int)(offsetof(LaneState<ENV>, toiEvents) / 4), upload_tables, init, reset, step,
+        using D = Dims<ENV>;
+        return EnvOps{lane_words<ENV>(), (int)(offsetof(LaneState<ENV>, toiEvents) / 4),
+                      {D::OBS, D::ACT, D::NDRAW, D::NA, D::NB, D::NF}, upload_tables, init, reset, step,
                       bodies, faults, counters, render, goals, debug_read, debug_progress};
     }
 };
@@ -439,7 +441,7 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_velbench(int n
     __shared__ Shared<0> sh;
     const int tid = threadIdx.x;
     EnvParams P{};
-    W w(sh, g_tables[0], P, tid);
+    W w(sh, g_table, P, tid);
     auto& is = sh.isl;
     // nc >= 100: a chain of nc - 100 contacts (contact i between bodies i and i + 1, all moving)
     const bool chain = nc >= 100;
@@ -472,7 +474,7 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_velbench(int n
 }
 }  // namespace
 hipError_t mrp::velbench_launch(const EnvTables* all, int nc, int pcount, int iters, int blocks, unsigned long long* d_out) {
-    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_tables), all, sizeof(EnvTables) * N_ENVS);
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_table), all, sizeof(EnvTables));
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_velbench, dim3(blocks), dim3(BLOCK), 0, nullptr, nc, pcount, iters, d_out);
     return hipGetLastError();

@@ -58,6 +58,7 @@ enum : int { DBG_STAMPS = 0, DBG_PMAX = 1, DBG_STEPMAX = 2, DBG_RT = 3, DBG_TRAC
 struct EnvOps {
     int words;                 // lane_words<ENV>()
     int counters_word;         // word offset of LaneState::toiEvents (followed by posIters)
+    int dims[6];               // Dims<ENV>: OBS, ACT, NDRAW, NA, NB, NF (mrp_create checks them against the tables)
     hipError_t (*upload_tables)(const EnvTables* all);   // all N_ENVS tables -> this unit's __constant__ copy
     void (*init)(hipStream_t, uint32_t* state, int nl);
     void (*reset)(hipStream_t, uint32_t* state, int nl, const uint8_t* mask, const double* draws, const float* actions,
@@ -76,13 +77,15 @@ struct EnvOps {
 };
 
 // defined in mrp_env<E>.hip
-extern const EnvOps g_env_ops_0, g_env_ops_1, g_env_ops_2, g_env_ops_3, g_env_ops_4, g_env_ops_5, g_env_ops_6;
+extern const EnvOps g_env_ops_0, g_env_ops_1, g_env_ops_2, g_env_ops_3, g_env_ops_4, g_env_ops_5, g_env_ops_6,
+    g_env_ops_7, g_env_ops_8, g_env_ops_9, g_env_ops_10, g_env_ops_11, g_env_ops_12, g_env_ops_13, g_env_ops_14;
 // defined in mrp_env0.hip: the lane-distributed velocity-sweep micro-benchmark (mrp_debug_velbench)
 hipError_t velbench_launch(const EnvTables* all, int nc, int pcount, int iters, int blocks, unsigned long long* d_out);
 
 inline const EnvOps* env_ops(int env_id) {
-    static const EnvOps* const t[N_ENVS] = {&g_env_ops_0, &g_env_ops_1, &g_env_ops_2, &g_env_ops_3,
-                                            &g_env_ops_4, &g_env_ops_5, &g_env_ops_6};
+    static const EnvOps* const t[N_ENVS] = {&g_env_ops_0,  &g_env_ops_1,  &g_env_ops_2,  &g_env_ops_3,  &g_env_ops_4,
+                                            &g_env_ops_5,  &g_env_ops_6,  &g_env_ops_7,  &g_env_ops_8,  &g_env_ops_9,
+                                            &g_env_ops_10, &g_env_ops_11, &g_env_ops_12, &g_env_ops_13, &g_env_ops_14};
     return env_id >= 0 && env_id < N_ENVS ? t[env_id] : nullptr;
 }
 

@@ -1,5 +1,5 @@
 // mrp_render.h -- batched rgb_array rendering of lanes straight from the SoA lane state
-// (SURVEY.md section 8f-3).  Included by mrp_lane.h after g_tables is declared
+// (SURVEY.md section 8f-3).  Included by mrp_lane.h after g_table is declared
 // (RenderArgs, RBLOCK and RPPT live in mrp_ops.h).
 //
 // Replaces the pyglet/OpenGL `render(mode='rgb_array')` of the reference:
@@ -46,6 +46,7 @@ __device__ inline void xf_point(float px, float py, float s, float c, float vx, 
 template <int ENV>
 __device__ inline void add_poly(Prim* P, int& n, const EnvTables& T, int f, float px, float py, float s, float c, uint32_t rgb) {
     #pragma clang fp contract(off)
+    if (n >= MAXPRIM) return;   // pool guard (the largest scene, 3 blocks, holds 46 primitives)
     Prim& q = P[n++];
     q.type = P_POLY; q.rgb = rgb; q.nv = T.shape[f].count;
     for (int i = 0; i < q.nv; ++i) xf_point(px, py, s, c, T.shape[f].v[i].x, T.shape[f].v[i].y, q.vx[i], q.vy[i]);
@@ -58,12 +59,14 @@ __device__ inline void add_poly(Prim* P, int& n, const EnvTables& T, int f, floa
 }
 __device__ inline void add_circle(Prim* P, int& n, float x, float y, float r, uint32_t rgb) {
     #pragma clang fp contract(off)
+    if (n >= MAXPRIM) return;
     Prim& q = P[n++];
     q.type = P_CIRCLE; q.rgb = rgb; q.a = x; q.b = y; q.c = r * r; q.nv = 0;
     q.bx0 = x - r - BPAD; q.bx1 = x + r + BPAD; q.by0 = y - r - BPAD; q.by1 = y + r + BPAD;
 }
 __device__ inline void add_rect(Prim* P, int& n, float xlo, float ylo, float xhi, float yhi, uint32_t rgb) {
     #pragma clang fp contract(off)
+    if (n >= MAXPRIM) return;
     Prim& q = P[n++];
     q.type = P_RECT; q.rgb = rgb; q.a = xlo; q.b = ylo; q.c = xhi; q.d = yhi; q.nv = 0;
     q.bx0 = xlo; q.by0 = ylo; q.bx1 = xhi; q.by1 = yhi;
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(RBLOCK) void k_render(const uint32_t* __restrict__ 
         np = 0;
         if (lane >= 0 && lane < n_lanes) {
             const LaneState<ENV>& S = *reinterpret_cast<const LaneState<ENV>*>(state + (size_t)lane * lane_words<ENV>());
-            np = build_scene<ENV>(S, g_tables[ENV], A, P);
+            np = build_scene<ENV>(S, g_table, A, P);
         }
     }
     __syncthreads();

@@ -161,18 +161,21 @@ static FixSpec box_fix(float hx, float hy, float cx, float cy, float density, fl
 bool build_tables(int env_id, EnvTables& t) {
     if (env_id < 0 || env_id >= N_ENVS) return false;
     std::memset(&t, 0, sizeof(t));
-    static const int NA[N_ENVS] = {2, 5, 2, 2, 2, 2, 2}, NB[N_ENVS] = {1, 1, 1, 1, 3, 1, 1};
-    static const int OBS[N_ENVS] = {28, 40, 39, 39, 69, 27, 27}, ACT[N_ENVS] = {6, 15, 4, 4, 4, 6, 6};
-    static const int NDRAW[N_ENVS] = {7, 13, 7, 7, 9, 7, 7};
-    static const int MAXSTEPS[N_ENVS] = {2000, 3000, 2000, 2000, 2000, 1500, 1500};
-    t.env_id = env_id; t.version = env_id < 2 ? 0 : (env_id < 5 ? 2 : 3);
-    t.n_agents = NA[env_id]; t.n_blocks = NB[env_id];
+    const EnvCfg& cfg = ENV_CFG[env_id];
+    const int na = cfg.n_agents, nb = cfg.n_blocks;
+    t.env_id = env_id; t.version = cfg.version;
+    t.n_agents = na; t.n_blocks = nb;
     t.n_dyn = t.n_agents + t.n_blocks; t.n_bodies = t.n_dyn + 4;
-    t.obs_dim = OBS[env_id]; t.act_dim = ACT[env_id]; t.n_draws = NDRAW[env_id]; t.max_steps = MAXSTEPS[env_id];
+    // action / spawn-draw layouts: multi_robot_puzzle_00.py:206,311-315,366-367 (3 action values per
+    // agent; block x, y, angle + agent x, y), _02.py:194,307-308,324,358-359 (2 per agent; block
+    // angles + agent x, y + goal x, y), core.py:136,212-215,231-232 (v3 as v0); obs_dim at the end
+    if (cfg.version == 2) { t.act_dim = 2 * na; t.n_draws = nb + 2 * na + 2; }
+    else { t.act_dim = 3 * na; t.n_draws = 3 + 2 * na; }
+    t.max_steps = cfg.max_steps;
     int nfix = 0;
     const double PI = 3.141592653589793;
     if (t.version == 0) {
-        const bool heavy = env_id == 1;
+        const bool heavy = cfg.heavy != 0;
         const double S = 2.0, scaled = heavy ? S / 2 : S, dense = heavy ? 5.0 * 2 : 5.0;
         FixSpec blk[2] = {box_fix((float)(1 / scaled), (float)(1 / scaled), 0.0f, (float)(-1 / scaled), (float)dense, (float)0.999),
                           box_fix((float)(3 / scaled), (float)(1 / scaled), 0.0f, (float)(1 / scaled), (float)dense, (float)0.999)};
@@ -204,7 +207,7 @@ bool build_tables(int env_id, EnvTables& t) {
         // RobotPuzzleBase: Block("T") at scale 0.5 (heavy: 1) density 5 (heavy: 10), friction 2.5,
         // damping 5 (blocks.py:70-90, core.py:204-225); Robot AGENT_POLY * 8, density 5,
         // friction 0.2, no damping (robot.py:34-44); walls as v0 (core.py:186-201)
-        const bool heavy = env_id == 6;
+        const bool heavy = cfg.heavy != 0;
         const double sc = heavy ? 1.0 : 0.5, dense = heavy ? 5.0 * 2 : 5.0;
         FixSpec blk[2] = {box_fix((float)(1 * sc), (float)(1 * sc), 0.0f, (float)(-1 * sc), (float)dense, 2.5f),
                           box_fix((float)(3 * sc), (float)(1 * sc), 0.0f, (float)(1 * sc), (float)dense, 2.5f)};
@@ -234,7 +237,7 @@ bool build_tables(int env_id, EnvTables& t) {
         for (int i = 0; i < t.n_agents; ++i) { t.draw_lo[k] = 1; t.draw_hi[k++] = vw / 3 - 2 * 1; t.draw_lo[k] = 1; t.draw_hi[k++] = vh - 1; }
         t.agent_angle = 0.0f;
     } else {
-        const bool heavy = env_id >= 3;
+        const bool heavy = cfg.heavy != 0;
         const float dense = (float)(heavy ? 20.0 : 1.56);
         const double vw = 1440 / 560.0, vh = 810 / 560.0;
         for (int b = 0; b < t.n_blocks; ++b) {
@@ -275,11 +278,17 @@ bool build_tables(int env_id, EnvTables& t) {
         }
     }
     t.n_fix = nfix;
+    // obs layouts: multi_robot_puzzle_00.py:188-200 (4 per agent, block 4 + its vertices),
+    // _02.py:178-188 (9 per agent, 4 + vertices per block, contact weight), core.py:121-132 (v3:
+    // 4 per agent, block 3 + vertices)
+    int nv = 0;
+    for (int b = 0; b < nb; ++b) nv += 2 * t.nverts[b];
+    t.obs_dim = cfg.version == 0 ? 4 * na + 4 + nv : (cfg.version == 3 ? 4 * na + 3 + nv : 9 * na + 4 * nb + nv + 1);
     return true;
 }
 
 void default_params(int env_id, EnvParams& p) {
-    if (env_id < 2 || env_id >= 5) {   // set_reward_params defaults multi_robot_puzzle_00.py:231-239, core.py:149-155
+    if (env_id < 0 || env_id >= N_ENVS || ENV_CFG[env_id].version != 2) {   // set_reward_params defaults multi_robot_puzzle_00.py:231-239, core.py:149-155
         p.w_dAgent = 10; p.w_agentDist = 0.1; p.w_dBlock = 50; p.w_blkDist = 0.025; p.scaled_epsilon = 25.0;
     } else {            // multi_robot_puzzle_02.py:216-225, EPSILON :58
         p.w_dAgent = 10; p.w_agentDist = 0.25; p.w_dBlock = 25; p.w_blkDist = 0.1; p.scaled_epsilon = 0.1;

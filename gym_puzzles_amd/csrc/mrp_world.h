@@ -18,6 +18,8 @@
 // SAH insertion, rotations) because its free list decides the proxy ids after a reset, and
 // proxy ids decide fixture A/B roles and the contact (= Gauss-Seidel) order.
 #pragma once
+#include <type_traits>
+
 #include "mrp_config.h"
 
 namespace mrp {
@@ -105,7 +107,10 @@ template <int ENV> struct alignas(16) LaneState {   // 16-B granules: moved with
     static constexpr int ND = D::NA + D::NB;
     static constexpr int C = D::CMAX;
     static constexpr int TN = tree_n<ENV>();
+    static constexpr int MOVE_N = move_n<ENV>();
+    using PMask = typename std::conditional<(TN <= 32), uint32_t, uint64_t>::type;   // one bit per proxy (tree node) id
     static_assert(D::NF < MOVE_N, "move buffer smaller than the proxy count");
+    static_assert(D::NA + D::NB + 4 <= MAXBODY && D::NF <= MAXF, "env tables too small for this env id");
     // dynamic bodies (blocks, then agents): transform, sweep, velocity, force accumulators
     float xpx[ND], xpy[ND], xs[ND], xc[ND];
     float c0x[ND], c0y[ND], cx[ND], cy[ND], a0[ND], a[ND], alpha0[ND];
@@ -214,7 +219,7 @@ template <int ENV> struct Shared {
     uint32_t smid[2];
     // broad phase: active proxy ids (ascending)
     int nprox;
-    uint32_t moved;
+    typename LS::PMask moved;
     int prox[LS::TN];
     // TOI scan bookkeeping
     int tn, np, toi_done, toi_fnc, toi_solve;
@@ -417,7 +422,7 @@ template <int ENV> struct World {
         }
     }
     __device__ __forceinline__ void buffer_move(int id) {
-        if (S.moveCount >= MOVE_N) { S.fault = MRP_FAULT_MOVE_BUFFER; return; }   // never in a valid world
+        if (S.moveCount >= LS::MOVE_N) { S.fault = MRP_FAULT_MOVE_BUFFER; return; }   // never in a valid world
         S.moveBuf[S.moveCount++] = id;
     }
     __device__ __forceinline__ void unbuffer_move(int id) { for (int i = 0; i < S.moveCount; ++i) if (S.moveBuf[i] == id) S.moveBuf[i] = NULLN; }
@@ -523,8 +528,8 @@ template <int ENV> struct World {
     // the order-sensitive AddPair calls run on thread 0 in sorted order.
     __device__ __forceinline__ void find_new_contacts_coop() {
         if (tid == 0) {
-            uint32_t moved = 0;
-            for (int i = 0; i < S.moveCount; ++i) if (S.moveBuf[i] != NULLN) moved |= 1u << S.moveBuf[i];
+            typename LS::PMask moved = 0;
+            for (int i = 0; i < S.moveCount; ++i) if (S.moveBuf[i] != NULLN) moved |= (typename LS::PMask)1 << S.moveBuf[i];
             S.moveCount = 0;
             int n = 0;
             if (moved)
@@ -534,7 +539,7 @@ template <int ENV> struct World {
         }
         __syncthreads();
         const int n = sh.nprox;
-        const uint32_t moved = sh.moved;
+        const typename LS::PMask moved = sh.moved;
         const int npairs = n * (n - 1) / 2;
         for (int p = tid; p < npairs; p += 64) {
             int i = 0, q = p;

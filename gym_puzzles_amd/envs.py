@@ -30,7 +30,7 @@ import numpy as np
 from ._native import (STATUS_AGENT_OOB, STATUS_BLOCK_OOB, STATUS_FAULT, STATUS_KIND_MASK, STATUS_NONFINITE,
                       STATUS_PUZZLE_COMPLETE, Batch)
 from .seeding import make_box, np_random
-from .spawn import reference_draws
+from .spawn import ENV_VERSION, V2_AGENT_IDS, reference_draws
 
 _DONE_STATUS = {STATUS_PUZZLE_COMPLETE: "puzzle complete!!", STATUS_AGENT_OOB: "agent out of bounds",
                 STATUS_BLOCK_OOB: "block out of bounds"}
@@ -108,7 +108,7 @@ class _MRPBase:
     # -- tuning hooks ------------------------------------------------------------------------
     def set_reward_params(self, agentDelta=10, agentDistance=None, blockDelta=None, blockDistance=None,
                           puzzleComp=10000, outOfBounds=1000, blkOutOfBounds=100):
-        v0 = self.env_id < 2
+        v0 = ENV_VERSION[self.env_id] == 0
         self.weight_deltaAgent = agentDelta
         self.weight_agent_dist = (0.1 if v0 else 0.25) if agentDistance is None else agentDistance
         self.weight_deltaBlock = (50 if v0 else 25) if blockDelta is None else blockDelta
@@ -121,7 +121,7 @@ class _MRPBase:
 
     def update_params(self, timestep, decay):
         self._b.update_params(timestep, decay)
-        if self.env_id >= 2:
+        if ENV_VERSION[self.env_id] == 2:
             self.shaped_bounds_penalty = self.out_of_bounds_penalty * decay ** (-timestep)
         self.shaped_blk_bounds_penalty = self.blk_out_of_bounds_penalty * decay ** (-timestep)
         self.shaped_puzzle_reward = self.puzzle_complete_reward * decay ** (-timestep)
@@ -129,7 +129,7 @@ class _MRPBase:
 
     def update_goal(self, epoch, nb_epochs):
         self._b.update_goal(epoch, nb_epochs)
-        self.scaled_epsilon = (25.0 if self.env_id < 2 else 0.1) * (2 - epoch / nb_epochs)
+        self.scaled_epsilon = (25.0 if ENV_VERSION[self.env_id] == 0 else 0.1) * (2 - epoch / nb_epochs)
 
     def get_deltaAgent(self):
         return self.weight_deltaAgent
@@ -145,7 +145,7 @@ class _MRPBase:
 
     # -- helpers -------------------------------------------------------------------------------
     def _needs_shaped(self):
-        return self.env_id >= 2
+        return ENV_VERSION[self.env_id] == 2
 
     def _obs_high(self):
         raise NotImplementedError
@@ -201,10 +201,16 @@ class MultiRobotPuzzle2(_MRPBase):
 
     def __init__(self, frameskip=1, num_agents=2, device: int = 0):
         # frameskip (multi_robot_puzzle_02.py:139,146,476-478) is a runtime parameter of the device
-        # step; num_agents sizes the obs / action layout and the per-lane pools, which the device
-        # build fixes at compile time per env id: only the registered value 2 has an instantiation
-        if num_agents != 2:
-            raise NotImplementedError("the device build instantiates num_agents=2 (the registered config)")
+        # step; num_agents (:151) sizes the obs / action layout and the per-lane pools, which the
+        # device build fixes at compile time: every count from 1 to 5 (Heavy-v0's agent count) has
+        # its own env id (include/mrp.h), the T block keeps its single-block layout
+        if type(self).env_id in (2, 3):
+            key = (int(self.heavy), int(num_agents))
+            if key not in V2_AGENT_IDS:
+                raise NotImplementedError(f"num_agents={num_agents}: the device build instantiates 1 to 5 agents")
+            self.env_id = V2_AGENT_IDS[key]
+        elif num_agents != 2:
+            raise NotImplementedError("the build-defined 3-block config is instantiated for num_agents=2")
         if int(frameskip) < 1:
             raise ValueError("frameskip must be >= 1")
         self.frameskip = int(frameskip)

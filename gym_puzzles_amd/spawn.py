@@ -24,19 +24,27 @@ _V2_SCALE, _V2_W, _V2_H, _V2_BORDER, _V2_GOAL_BORDER = 140.0 * 4, 1440, 810, 0.3
 # v3 constants (core.py:16-19, 97-98)
 _V3_SCALE, _V3_W, _V3_H, _V3_BORDER = 30.0, 640, 480, 1
 
-N_AGENTS = {0: 2, 1: 5, 2: 2, 3: 2, 4: 2, 5: 2, 6: 2}
-N_BLOCKS = {0: 1, 1: 1, 2: 1, 3: 1, 4: 3, 5: 1, 6: 1}
+# env id -> (version, agents, blocks, heavy) (csrc/mrp_config.h ENV_CFG); ids 7-10 / 11-14 are
+# MultiRobotPuzzle2 / MultiRobotPuzzleHeavy2 constructed with num_agents = 1, 3, 4, 5
+ENV_CFG = {0: (0, 2, 1, 0), 1: (0, 5, 1, 1), 2: (2, 2, 1, 0), 3: (2, 2, 1, 1), 4: (2, 2, 3, 1), 5: (3, 2, 1, 0), 6: (3, 2, 1, 1),
+           7: (2, 1, 1, 0), 8: (2, 3, 1, 0), 9: (2, 4, 1, 0), 10: (2, 5, 1, 0),
+           11: (2, 1, 1, 1), 12: (2, 3, 1, 1), 13: (2, 4, 1, 1), 14: (2, 5, 1, 1)}
+ENV_VERSION = {e: c[0] for e, c in ENV_CFG.items()}
+N_AGENTS = {e: c[1] for e, c in ENV_CFG.items()}
+N_BLOCKS = {e: c[2] for e, c in ENV_CFG.items()}
+# MultiRobotPuzzle2(num_agents=N) / MultiRobotPuzzleHeavy2(num_agents=N) -> env id
+V2_AGENT_IDS = {(h, c[1]): e for e, c in ENV_CFG.items() if c[0] == 2 and c[2] == 1 for h in (c[3],)}
 
 
 def draw_bounds(env_id: int):
     """(low, high) of every uniform draw of one reset, in call order."""
     b = []
-    if env_id in (0, 1):
+    if ENV_VERSION[env_id] == 0:
         xr = (_V0_BORDER, _V0_W / _V0_SCALE - _V0_BORDER)
         yr = (_V0_BORDER, _V0_H / _V0_SCALE - _V0_BORDER)
         b += [xr, yr, (0, 2 * np.pi)]
         b += [xr, yr] * N_AGENTS[env_id]
-    elif env_id in (5, 6):
+    elif ENV_VERSION[env_id] == 3:
         b += [(_V3_W / _V3_SCALE / 3 + 2 * _V3_BORDER, _V3_W / _V3_SCALE * 2 / 3 - 2 * _V3_BORDER),
               (3 * _V3_BORDER, _V3_H / _V3_SCALE - 3 * _V3_BORDER), (0, 2 * np.pi)]
         b += [(_V3_BORDER, _V3_W / _V3_SCALE / 3 - 2 * _V3_BORDER), (_V3_BORDER, _V3_H / _V3_SCALE - _V3_BORDER)] * N_AGENTS[env_id]

@@ -22,6 +22,7 @@ from __future__ import annotations
 import numpy as np
 
 from ._native import ENV_IDS, STATUS_FAULT, STATUS_NONFINITE, Batch, env_dims
+from .spawn import ENV_CFG, V2_AGENT_IDS
 from .seeding import make_box
 
 try:   # SB3 1.x/2.x: VecEnv(num_envs, observation_space, action_space)
@@ -48,8 +49,15 @@ def _lane_flags(batch: Batch, status: np.ndarray, infos: list) -> None:
 
 class MultiRobotPuzzleVecEnv(_VecEnvBase):
     def __init__(self, env_id, num_envs: int, device: int = 0, seed: int = 0, lane_offset: int = 0,
-                 max_episode_steps: int | None = None, frameskip: int = 1):
+                 max_episode_steps: int | None = None, frameskip: int = 1, num_agents: int | None = None):
         self.env_index = _ID[env_id] if isinstance(env_id, str) else int(env_id)
+        if num_agents is not None and num_agents != env_dims(self.env_index)["n_agents"]:
+            # MultiRobotPuzzle2 / Heavy2(num_agents=N) (multi_robot_puzzle_02.py:139): the env id of that count
+            cfg = ENV_CFG[self.env_index]
+            key = (cfg[3], int(num_agents))
+            if cfg[0] != 2 or cfg[2] != 1 or key not in V2_AGENT_IDS:
+                raise NotImplementedError(f"num_agents={num_agents} is not instantiated for env {env_id!r}")
+            self.env_index = V2_AGENT_IDS[key]
         d = env_dims(self.env_index)
         self.num_envs = num_envs
         self.device = device

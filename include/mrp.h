@@ -22,6 +22,8 @@
  *          4 MultiRobotPuzzleHeavy-v2 with the build-defined 3-block square
  *          5 MultiRobotPuzzle-v3       (gym_puzzles/__init__.py:31-35, core.py:77 RobotPuzzleBase)
  *          6 MultiRobotPuzzle-v3 constructed with heavy=True (gym_puzzles/tests/test_env.py:12)
+ *          7-10  MultiRobotPuzzle2(num_agents=1, 3, 4, 5)      (multi_robot_puzzle_02.py:139,151,354)
+ *          11-14 MultiRobotPuzzleHeavy2(num_agents=1, 3, 4, 5) (multi_robot_puzzle_02.py:711)
  */
 #ifndef MRP_H
 #define MRP_H
@@ -52,7 +54,8 @@ typedef struct mrp_ctx mrp_ctx;
 
 /* Static dimensions of an env id: observation_space / action_space shapes
  * (multi_robot_puzzle_00.py:186-207, _02.py:174-195), number of spawn draws per reset,
- * agents, blocks and the TimeLimit max_episode_steps (gym_puzzles/__init__.py:6-27). */
+ * agents, blocks and the TimeLimit max_episode_steps (gym_puzzles/__init__.py:6-27).
+ * MRP_E_STATE if the library's compiled layout of the env disagrees with its tables (a build defect). */
 int mrp_env_dims(int env_id, int* obs_dim, int* act_dim, int* n_draws, int* n_agents, int* n_blocks,
                  int* max_episode_steps);
 

@@ -57,7 +57,8 @@ double or_rng_u01(uint64_t seed, uint64_t lane, uint64_t stream, uint64_t counte
 
 /* ---------------------------------------------------------------- configs (BASELINE.json configs) */
 typedef struct { int version, n_agents, n_blocks, heavy, obs_dim, act_dim, n_draws, max_steps; } Cfg;
-static const Cfg CFGS[7] = {
+#define N_CFGS 15
+static const Cfg CFGS[N_CFGS] = {
     {0, 2, 1, 0, 28, 6, 7, 2000},   /* MultiRobotPuzzle-v0        __init__.py:3-8 */
     {0, 5, 1, 1, 40, 15, 13, 3000}, /* MultiRobotPuzzleHeavy-v0   __init__.py:10-15 */
     {2, 2, 1, 0, 39, 4, 7, 2000},   /* MultiRobotPuzzle-v2        __init__.py:17-22 */
@@ -65,8 +66,12 @@ static const Cfg CFGS[7] = {
     {2, 2, 3, 1, 69, 4, 9, 2000},   /* Heavy-v2, 3-block square (build-defined) */
     {3, 2, 1, 0, 27, 6, 7, 1500},   /* MultiRobotPuzzle-v3 (RobotPuzzleBase)  __init__.py:31-35 */
     {3, 2, 1, 1, 27, 6, 7, 1500},   /* MultiRobotPuzzle-v3 with heavy=True (tests/test_env.py:12) */
+    /* MultiRobotPuzzle2(num_agents=N) / MultiRobotPuzzleHeavy2(num_agents=N), _02.py:139,151,178-194:
+     * obs 9 N + 4 + 16 + 1, action 2 N, draws 1 + 2 N + 2 */
+    {2, 1, 1, 0, 30, 2, 5, 2000}, {2, 3, 1, 0, 48, 6, 9, 2000}, {2, 4, 1, 0, 57, 8, 11, 2000}, {2, 5, 1, 0, 66, 10, 13, 2000},
+    {2, 1, 1, 1, 30, 2, 5, 2000}, {2, 3, 1, 1, 48, 6, 9, 2000}, {2, 4, 1, 1, 57, 8, 11, 2000}, {2, 5, 1, 1, 66, 10, 13, 2000},
 };
-static int valid(int id) { return id >= 0 && id < 7; }
+static int valid(int id) { return id >= 0 && id < N_CFGS; }
 int or_obs_dim(int id) { return valid(id) ? CFGS[id].obs_dim : -1; }
 int or_act_dim(int id) { return valid(id) ? CFGS[id].act_dim : -1; }
 int or_n_draws(int id) { return valid(id) ? CFGS[id].n_draws : -1; }

@@ -21,7 +21,8 @@ WHITE, GREY, WALL, BLUE = (255, 255, 255), (128, 128, 128), (51, 51, 51), (58, 1
 
 
 def _v2(env_id: int) -> bool:
-    return 2 <= env_id <= 4
+    from oracle.oracle import ENV_VERSION
+    return ENV_VERSION[env_id] == 2
 
 
 def _viewport(env_id: int):
@@ -43,7 +44,8 @@ def _xf(px, py, s, c, vx, vy):
 def build_scene(env_id, shapes, n_agents, n_blocks, xf, centers, goals, scaled_epsilon=0.1):
     """Display list of one lane.  xf: [ND, 4] f32 (p.x, p.y, sin, cos) of the dynamic bodies
     (blocks, agents); centers: [ND, 2] f32 worldCenter; goals: [NB, 3] f64 block_final_pos."""
-    v0, v3 = env_id <= 1, env_id >= 5
+    from oracle.oracle import ENV_VERSION
+    v0, v3 = ENV_VERSION[env_id] == 0, ENV_VERSION[env_id] == 3
     ww, wh, lw, gscale = _viewport(env_id)
     lw = f32(lw)
     nd = n_agents + n_blocks

@@ -6,12 +6,18 @@ from __future__ import annotations
 
 # Dims<ENV> (mrp_config.h): NA, NB, NF, CMAX
 DIMS = {0: (2, 1, 8, 21), 1: (5, 1, 11, 48), 2: (2, 1, 12, 53), 3: (2, 1, 12, 53), 4: (2, 3, 15, 91),
-        5: (2, 1, 8, 21), 6: (2, 1, 8, 21)}
-MOVE_N = 16
+        5: (2, 1, 8, 21), 6: (2, 1, 8, 21),
+        # MultiRobotPuzzle2 / Heavy2 with num_agents = 1, 3, 4, 5 (DimsV2<N>)
+        7: (1, 1, 9, 26), 8: (3, 1, 15, 89), 9: (4, 1, 18, 134), 10: (5, 1, 21, 188),
+        11: (1, 1, 9, 26), 12: (3, 1, 15, 89), 13: (4, 1, 18, 134), 14: (5, 1, 21, 188)}
 
 
 def tree_n(nf: int) -> int:
-    return 16 if 2 * nf - 1 <= 16 else 32
+    return 16 if 2 * nf - 1 <= 16 else (32 if 2 * nf - 1 <= 32 else 64)
+
+
+def move_n(nf: int) -> int:
+    return 16 if nf < 16 else 32
 
 
 def fields(env_id: int):
@@ -26,7 +32,7 @@ def fields(env_id: int):
         f.append((n, tn))
     for n in ("root", "freeList", "nodeCount", "moveCount"):
         f.append((n, 1))
-    f.append(("moveBuf", MOVE_N))
+    f.append(("moveBuf", move_n(nf)))
     for n in ("cHead", "cFree", "cCount", "cHW"):
         f.append((n, 1))
     for n in ("cnext", "cprev", "cfa", "cfb", "cflags", "ctoiCount", "ctoi", "cfric", "mpc", "mtype",

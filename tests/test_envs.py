@@ -11,6 +11,8 @@ import os
 import numpy as np
 import pytest
 
+from gym_puzzles_amd.spawn import reference_draws
+
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
@@ -162,6 +164,55 @@ def test_single_env_spaces_and_step(gpu_lib, name, obs_dim, act_dim):
     for _ in range(20):
         o, r, d, info = env.step(env.action_space.sample())
         assert np.isfinite(o).all() and np.isfinite(r)
+    env.close()
+
+
+def test_num_agents_maps_to_its_env_id():
+    """MultiRobotPuzzle2 / MultiRobotPuzzleHeavy2(num_agents=N) (multi_robot_puzzle_02.py:139) for N = 1..5:
+    each count has its own env id whose tables hold N agents; other counts raise before any device work."""
+    from gym_puzzles_amd import envs
+    from gym_puzzles_amd.spawn import ENV_CFG, V2_AGENT_IDS, draw_bounds
+    for heavy in (0, 1):
+        for n in range(1, 6):
+            e = V2_AGENT_IDS[(heavy, n)]
+            assert ENV_CFG[e] == (2, n, 1, heavy)
+            assert len(draw_bounds(e)) == 1 + 2 * n + 2
+    for cls in (envs.MultiRobotPuzzle2, envs.MultiRobotPuzzleHeavy2):
+        with pytest.raises(NotImplementedError):
+            cls(num_agents=6)
+        with pytest.raises(NotImplementedError):
+            cls(num_agents=0)
+    with pytest.raises(NotImplementedError):
+        envs.MultiRobotPuzzleHeavy2ThreeBlock(num_agents=3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("heavy", [False, True])
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5])
+def test_multi_robot_puzzle2_num_agents(gpu_lib, oracle_lib, heavy, n):
+    """The constructor's spaces follow _02.py:178-194 (9 obs per agent + block 4 + 16 vertices + contact
+    weight; 2 action values per agent), and its steps equal the oracle of the same agent count bit for bit."""
+    from gym_puzzles_amd import MultiRobotPuzzle2, MultiRobotPuzzleHeavy2
+    from oracle import oracle
+    env = (MultiRobotPuzzleHeavy2 if heavy else MultiRobotPuzzle2)(num_agents=n)
+    assert env.num_agents == n
+    assert env.observation_space.shape == (9 * n + 21,) and env.action_space.shape == (2 * n,)
+    assert env.observation_space.high[2] == np.float32(2 * np.pi) and env.observation_space.high[9 * n + 2] == np.float32(2 * np.pi)
+    env.update_params(0, 1.0)
+    rs = np.random.RandomState(5 + n)
+    draws = reference_draws(env.env_id, rs)
+    a0 = rs.uniform(-1, 1, 2 * n).astype(np.float32)
+    obs = env._b.reset(draws[None], a0[None])[0].copy()
+    o = oracle.OracleEnv(env.env_id)
+    o.set_shaped(1000.0, 100.0, 10000.0)
+    assert np.array_equal(obs, o.reset(draws, a0).astype(np.float32))
+    for _ in range(40):
+        a = rs.uniform(-1, 1, 2 * n).astype(np.float32)
+        ob, r, d, _ = env.step(a)
+        ob_o, r_o, d_o, _ = o.step(a)
+        assert np.array_equal(ob.astype(np.float32), ob_o.astype(np.float32)) and np.float32(r) == np.float32(r_o)
+        if d:
+            break
     env.close()
 
 

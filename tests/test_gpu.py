@@ -18,6 +18,8 @@ from gym_puzzles_amd.spawn import draw_bounds, reference_draws
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 ENVS = range(7)
+# MultiRobotPuzzle2 / MultiRobotPuzzleHeavy2(num_agents = 1, 3, 4, 5) (multi_robot_puzzle_02.py:139)
+AGENT_VARIANTS = range(7, 15)
 
 
 @pytest.fixture(scope="module")
@@ -34,7 +36,7 @@ def _eq(name, g, c):
         raise AssertionError(f"{name}: {int(bad.sum())} elements differ, first at {i}: gpu {g[i]!r} oracle {c[i]!r}")
 
 
-@pytest.mark.parametrize("env_id", ENVS)
+@pytest.mark.parametrize("env_id", list(ENVS) + list(AGENT_VARIANTS))
 def test_step_parity_host_inputs(gpu_lib, orc, env_id):
     """64 lanes x 200 steps with host spawns/actions; finished lanes reset through the mask."""
     from gym_puzzles_amd import Batch
@@ -123,13 +125,13 @@ def test_reference_test_flow_v0_seed17(gpu_lib):
     b.close()
 
 
-@pytest.mark.parametrize("env_id", ENVS)
+@pytest.mark.parametrize("env_id", list(ENVS) + list(AGENT_VARIANTS))
 def test_device_autoreset_full_size(gpu_lib, orc, env_id):
-    """BASELINE.json-size batch (4096 lanes) on the device-input path: counter-RNG spawns and
-    actions, TimeLimit 64 so every lane auto-resets several times; final body state and per-lane
-    reward sums must equal the oracle's batch runner bit for bit."""
+    """BASELINE.json-size batch (4096 lanes; 1024 for the num_agents variants) on the device-input
+    path: counter-RNG spawns and actions, TimeLimit 64 so every lane auto-resets several times; final
+    body state and per-lane reward sums must equal the oracle's batch runner bit for bit."""
     from gym_puzzles_amd import Batch
-    lanes, steps, limit = 4096, 200, 64
+    lanes, steps, limit = (4096 if env_id in ENVS else 1024), 200, 64
     b = Batch(env_id, lanes, seed=17)
     b.set_auto_reset(True)
     b.set_time_limit(limit)
@@ -292,14 +294,14 @@ def test_costliest_first_schedule_changes_nothing(gpu_lib):
     b.close()
 
 
-@pytest.mark.parametrize("env_id", ENVS)
+@pytest.mark.parametrize("env_id", list(ENVS) + list(AGENT_VARIANTS))
 def test_whole_episode_soak(gpu_lib, orc, env_id):
     """One whole episode at the registered TimeLimit (2000 / 3000 / 1500 steps) plus 50 steps of
     the next, on the device-RNG + auto-reset path the bench runs: every lane reaches its TimeLimit
     reset (or an earlier done), no loop guard trips, every observation stays finite, and the final
     body state and per-lane reward sums equal the oracle's batch runner bit for bit."""
     from gym_puzzles_amd import Batch
-    lanes = 4096 if env_id in (0, 5) else 1024
+    lanes = 4096 if env_id in (0, 5) else (1024 if env_id in ENVS else 256)
     b = Batch(env_id, lanes, seed=23)
     steps = b.max_episode_steps + 50
     b.set_auto_reset(True)

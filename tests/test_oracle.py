@@ -20,7 +20,7 @@ import os
 import numpy as np
 import pytest
 
-from gym_puzzles_amd.spawn import draw_bounds, reference_draws
+from gym_puzzles_amd.spawn import ENV_CFG, draw_bounds, reference_draws
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -76,17 +76,18 @@ def _expected_masses(env_id):
                          _poly_mass(_box(1.5 * s, 0.5 * s, 0, 0.5 * s), 5.0 * (2 if env_id == 1 else 1))])
         agent = (1.0, np.zeros(2), 0.0)    # zero density -> mass 1, I 0 (Box2D ResetMassData)
         return [blk] + [agent] * (2 if env_id == 0 else 5)
-    dens = 1.56 if env_id == 2 else 20.0
+    _, na, nb, heavy = ENV_CFG[env_id]
+    dens = 20.0 if heavy else 1.56
     t = _compound([_poly_mass(_box(0.1, 0.1, 0, -0.1), dens), _poly_mass(_box(0.3, 0.1, 0, 0.1), dens)])
     agent = _poly_mass(AGENT_V2, 17.3)
-    if env_id in (2, 3):
-        return [t, agent, agent]
+    if nb == 1:   # MultiRobotPuzzle2(num_agents=na): the T block, then na agents (_02.py:313-378)
+        return [t] + [agent] * na
     l_blk = _compound([_poly_mass(_box(0.1, 0.1, 0.1, 0.05), dens), _poly_mass(_box(0.1, 0.2, -0.1, -0.05), dens)])
     i_blk = _poly_mass(_box(0.1, 0.2), dens)
     return [t, l_blk, i_blk, agent, agent]
 
 
-@pytest.mark.parametrize("env_id", range(7))
+@pytest.mark.parametrize("env_id", range(15))
 def test_mass_known_answers(orc, env_id):
     e = orc.OracleEnv(env_id)
     e.reset(reference_draws(env_id, np.random.RandomState(17)), np.zeros(e.act_dim, np.float32))
@@ -351,24 +352,29 @@ def test_batch_run_lane_offset_invariance(orc):
 # register / lane solvers need <= 64).  Box2D grows these dynamically; the oracle does too and
 # records its high-water marks, so a long synthetic rollout shows the fixed pools are never
 # exceeded (an overrun on the device would corrupt the lane's LDS instead of failing).
-POOLS = {e: {"contacts": c, "tree_node_id": (16 if 2 * nf - 1 <= 16 else 32) - 1, "move_buffer": 16,
-             "island_bodies": na + nb + 4, "island_contacts": min(c, 64), "toi_island_bodies": na + nb + 4,
-             "toi_island_contacts": min(c, 32)}
-         for e, (na, nb, nf, c) in {0: (2, 1, 8, 21), 1: (5, 1, 11, 48), 2: (2, 1, 12, 53), 3: (2, 1, 12, 53),
-                                    4: (2, 3, 15, 91), 5: (2, 1, 8, 21), 6: (2, 1, 8, 21)}.items()}
+def _pools():
+    from lane_layout import DIMS, move_n, tree_n
+    return {e: {"contacts": c, "tree_node_id": tree_n(nf) - 1, "move_buffer": move_n(nf),
+                "island_bodies": na + nb + 4, "island_contacts": min(c, 64), "toi_island_bodies": na + nb + 4,
+                "toi_island_contacts": min(c, 32)}
+            for e, (na, nb, nf, c) in DIMS.items()}
 
 
-@pytest.mark.parametrize("env_id", range(7))
+POOLS = _pools()
+
+
+@pytest.mark.parametrize("env_id", range(15))
 def test_device_pools_hold_the_oracle_high_water_marks(oracle_lib, env_id):
     from gym_puzzles_amd.spawn import draw_bounds
     from oracle.oracle import batch_capacity
-    caps = batch_capacity(env_id, 1024, 300, 41, draw_bounds(env_id), threads=min(8, os.cpu_count() or 1), max_steps=60)
+    lanes = 1024 if env_id < 7 else 256   # the num_agents variants: fewer lanes, same 300-step rollout
+    caps = batch_capacity(env_id, lanes, 300, 41, draw_bounds(env_id), threads=min(8, os.cpu_count() or 1), max_steps=60)
     for k, lim in POOLS[env_id].items():
         assert caps[k] <= lim, (k, caps[k], lim)
-    assert caps["tree_node_id"] < 32 and caps["move_buffer"] >= 1 and caps["contacts"] >= 1
+    assert caps["move_buffer"] >= 1 and caps["contacts"] >= 1
 
 
-@pytest.mark.parametrize("env_id", range(7))
+@pytest.mark.parametrize("env_id", range(15))
 def test_oracle_under_asan_ubsan(env_id):
     """The oracle's sources built with AddressSanitizer + UBSan (make -C oracle asan, every finding
     fatal) run the synthetic workload of every env id cleanly: 64 lanes x 500 steps, TimeLimit 60

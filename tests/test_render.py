@@ -10,9 +10,10 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
+from gym_puzzles_amd.spawn import ENV_VERSION
 from oracle import render_ref
 
-ENVS = range(7)
+ENVS = list(range(7)) + [7, 10, 14]   # num_agents variants 1 and 5 (light / heavy)
 
 
 def _dims(env_id):
@@ -62,7 +63,7 @@ def test_render_parity(gpu_lib, env_id):
     from gym_puzzles_amd import Batch
     from gym_puzzles_amd._native import shapes
     b = Batch(env_id, 4, seed=123)
-    v2 = 2 <= env_id <= 4
+    v2 = ENV_VERSION[env_id] == 2
     if v2:
         b.update_params(0, 1.0)
         b.update_goal(0, 1)   # scaled_epsilon = 0.1 * 2
