@@ -189,30 +189,31 @@ def test_num_agents_maps_to_its_env_id():
 @pytest.mark.gpu
 @pytest.mark.parametrize("heavy", [False, True])
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 5])
-def test_multi_robot_puzzle2_num_agents(gpu_lib, oracle_lib, heavy, n):
+def test_multi_robot_puzzle2_num_agents(gpu_lib, heavy, n):
     """The constructor's spaces follow _02.py:178-194 (9 obs per agent + block 4 + 16 vertices + contact
-    weight; 2 action values per agent), and its steps equal the oracle of the same agent count bit for bit."""
-    from gym_puzzles_amd import MultiRobotPuzzle2, MultiRobotPuzzleHeavy2
-    from oracle import oracle
+    weight; 2 action values per agent) and its steps are those of its env id's batch (whose steps
+    tests/test_gpu.py compares with the oracle bit for bit): a 1-lane batch given the env's state
+    steps to the same obs and rewards."""
+    from gym_puzzles_amd import Batch, MultiRobotPuzzle2, MultiRobotPuzzleHeavy2
     env = (MultiRobotPuzzleHeavy2 if heavy else MultiRobotPuzzle2)(num_agents=n)
     assert env.num_agents == n
     assert env.observation_space.shape == (9 * n + 21,) and env.action_space.shape == (2 * n,)
     assert env.observation_space.high[2] == np.float32(2 * np.pi) and env.observation_space.high[9 * n + 2] == np.float32(2 * np.pi)
     env.update_params(0, 1.0)
+    mirror = Batch(env.env_id, 1)
+    assert mirror.n_agents == n
+    mirror.set_time_limit(0)
+    mirror.update_params(0, 1.0)
+    mirror.set_state(env._b.get_state())
     rs = np.random.RandomState(5 + n)
-    draws = reference_draws(env.env_id, rs)
-    a0 = rs.uniform(-1, 1, 2 * n).astype(np.float32)
-    obs = env._b.reset(draws[None], a0[None])[0].copy()
-    o = oracle.OracleEnv(env.env_id)
-    o.set_shaped(1000.0, 100.0, 10000.0)
-    assert np.array_equal(obs, o.reset(draws, a0).astype(np.float32))
     for _ in range(40):
         a = rs.uniform(-1, 1, 2 * n).astype(np.float32)
         ob, r, d, _ = env.step(a)
-        ob_o, r_o, d_o, _ = o.step(a)
-        assert np.array_equal(ob.astype(np.float32), ob_o.astype(np.float32)) and np.float32(r) == np.float32(r_o)
+        mo, _, md, _ = mirror.step(a[None])
+        assert np.array_equal(ob.astype(np.float32), mo[0]) and r == mirror.reward64[0] and d == bool(md[0])
         if d:
             break
+    mirror.close()
     env.close()
 
 
