@@ -34,6 +34,10 @@ ENV_IDS = {
     "MultiRobotPuzzle-v2-agents1": 7, "MultiRobotPuzzle-v2-agents3": 8, "MultiRobotPuzzle-v2-agents4": 9,
     "MultiRobotPuzzle-v2-agents5": 10, "MultiRobotPuzzleHeavy-v2-agents1": 11, "MultiRobotPuzzleHeavy-v2-agents3": 12,
     "MultiRobotPuzzleHeavy-v2-agents4": 13, "MultiRobotPuzzleHeavy-v2-agents5": 14,
+    # RobotPuzzleBase(num_agents=N[, heavy=True]) (core.py:86-106)
+    "MultiRobotPuzzle-v3-agents1": 15, "MultiRobotPuzzle-v3-agents3": 16, "MultiRobotPuzzle-v3-agents4": 17,
+    "MultiRobotPuzzle-v3-agents5": 18, "MultiRobotPuzzle-v3-heavy-agents1": 19, "MultiRobotPuzzle-v3-heavy-agents3": 20,
+    "MultiRobotPuzzle-v3-heavy-agents4": 21, "MultiRobotPuzzle-v3-heavy-agents5": 22,
 }
 MAXF = 24   # csrc/mrp_config.h: fixtures per env (mrp_shapes fills MAXF rows)
 

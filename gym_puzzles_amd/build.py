@@ -17,7 +17,7 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmrp.so")
-N_ENVS = 15   # csrc/mrp_config.h N_ENVS: one translation unit per env id
+N_ENVS = 23   # csrc/mrp_config.h N_ENVS: one translation unit per env id
 SOURCES = ([os.path.join(CSRC, "mrp_kernels.hip"), os.path.join(CSRC, "mrp_tables.cpp"), os.path.join(CSRC, "mrp_norm.hip")]
            + [os.path.join(CSRC, f"mrp_env{e}.hip") for e in range(N_ENVS)])
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("mrp_math.h", "mrp_config.h", "mrp_world.h", "mrp_env.h", "mrp_tables.h",

@@ -6,7 +6,8 @@
 // 3-block square, 5 MultiRobotPuzzle-v3 (RobotPuzzleBase,
 // core.py), 6 v3 constructed with heavy=True (tests/test_env.py:12), 7-10 MultiRobotPuzzle2
 // constructed with num_agents = 1, 3, 4, 5 and 11-14 MultiRobotPuzzleHeavy2 with the same
-// agent counts (multi_robot_puzzle_02.py:139,151,354).
+// agent counts (multi_robot_puzzle_02.py:139,151,354), 15-18 / 19-22 RobotPuzzleBase(num_agents =
+// 1, 3, 4, 5) with heavy False / True (core.py:86-106).
 #pragma once
 #include "mrp_math.h"
 
@@ -46,9 +47,25 @@ template <> struct Dims<11> : DimsV2<1> {};
 template <> struct Dims<12> : DimsV2<3> {};
 template <> struct Dims<13> : DimsV2<4> {};
 template <> struct Dims<14> : DimsV2<5> {};
+// RobotPuzzleBase(num_agents = N) (core.py:88,106,230): one T block (2 fixtures), N Robots (1 fixture), 4 walls
+template <int N> struct DimsV3 {
+    static constexpr int DF = 2 + N;
+    static constexpr int V = 3, NA = N, NB = 1, NF = DF + 4, CMAX = DF * (DF - 1) / 2 - 1 + 4 * DF,
+                         OBS = 4 * N + 3 + 16, ACT = 3 * N, NDRAW = 3 + 2 * N;
+};
+template <> struct Dims<15> : DimsV3<1> {};
+template <> struct Dims<16> : DimsV3<3> {};
+template <> struct Dims<17> : DimsV3<4> {};
+template <> struct Dims<18> : DimsV3<5> {};
+template <> struct Dims<19> : DimsV3<1> {};
+template <> struct Dims<20> : DimsV3<3> {};
+template <> struct Dims<21> : DimsV3<4> {};
+template <> struct Dims<22> : DimsV3<5> {};
 static_assert(DimsV2<2>::CMAX == Dims<2>::CMAX && DimsV2<2>::OBS == Dims<2>::OBS && DimsV2<2>::NF == Dims<2>::NF &&
               DimsV2<2>::NDRAW == Dims<2>::NDRAW, "DimsV2 restates the registered v2 layout");
-constexpr int N_ENVS = 15;
+static_assert(DimsV3<2>::CMAX == Dims<5>::CMAX && DimsV3<2>::OBS == Dims<5>::OBS && DimsV3<2>::NF == Dims<5>::NF &&
+              DimsV3<2>::NDRAW == Dims<5>::NDRAW && DimsV3<2>::ACT == Dims<5>::ACT, "DimsV3 restates the v3 layout");
+constexpr int N_ENVS = 23;
 
 // Per env id: version (0 v0, 2 v2, 3 v3), agents, blocks, heavy block, registered TimeLimit.
 struct EnvCfg { int version, n_agents, n_blocks, heavy, max_steps; };
@@ -57,6 +74,8 @@ constexpr EnvCfg ENV_CFG[N_ENVS] = {
     {3, 2, 1, 0, 1500}, {3, 2, 1, 1, 1500},
     {2, 1, 1, 0, 2000}, {2, 3, 1, 0, 2000}, {2, 4, 1, 0, 2000}, {2, 5, 1, 0, 2000},
     {2, 1, 1, 1, 2000}, {2, 3, 1, 1, 2000}, {2, 4, 1, 1, 2000}, {2, 5, 1, 1, 2000},
+    {3, 1, 1, 0, 1500}, {3, 3, 1, 0, 1500}, {3, 4, 1, 0, 1500}, {3, 5, 1, 0, 1500},
+    {3, 1, 1, 1, 1500}, {3, 3, 1, 1, 1500}, {3, 4, 1, 1, 1500}, {3, 5, 1, 1, 1500},
 };
 
 // Node pool of a lane's dynamic tree.  b2DynamicTree starts at 16 nodes and doubles only when

@@ -30,7 +30,7 @@ import numpy as np
 from ._native import (STATUS_AGENT_OOB, STATUS_BLOCK_OOB, STATUS_FAULT, STATUS_KIND_MASK, STATUS_NONFINITE,
                       STATUS_PUZZLE_COMPLETE, Batch)
 from .seeding import make_box, np_random
-from .spawn import ENV_VERSION, V2_AGENT_IDS, reference_draws
+from .spawn import ENV_VERSION, V2_AGENT_IDS, V3_AGENT_IDS, reference_draws
 
 _DONE_STATUS = {STATUS_PUZZLE_COMPLETE: "puzzle complete!!", STATUS_AGENT_OOB: "agent out of bounds",
                 STATUS_BLOCK_OOB: "block out of bounds"}
@@ -248,9 +248,14 @@ class RobotPuzzleBase(_MRPBase):
 
     def __init__(self, num_agents: int = 2, goal_velocity: float = 1.5, block_density: float = 5.0,
                  heavy: bool = False, hardmode: bool = False, device: int = 0):
-        if num_agents != 2:
-            raise NotImplementedError("the device build covers num_agents=2 (the registered config)")
-        self.env_id = 6 if heavy else 5
+        # num_agents (core.py:88,106,230) sizes the obs / action layout and the per-lane pools: every
+        # count from 1 to 5 has its own env id (include/mrp.h); goal_velocity, block_density and
+        # hardmode are stored but never read by the reference (core.py:100-102; heavy picks the block)
+        key = (int(bool(heavy)), int(num_agents))
+        if key not in V3_AGENT_IDS:
+            raise NotImplementedError(f"num_agents={num_agents}: the device build instantiates 1 to 5 agents")
+        self.env_id = V3_AGENT_IDS[key]
+        self.block_density = block_density
         self.goal_velocity = goal_velocity
         self.heavy = heavy
         self.hardmode = hardmode

@@ -25,15 +25,20 @@ _V2_SCALE, _V2_W, _V2_H, _V2_BORDER, _V2_GOAL_BORDER = 140.0 * 4, 1440, 810, 0.3
 _V3_SCALE, _V3_W, _V3_H, _V3_BORDER = 30.0, 640, 480, 1
 
 # env id -> (version, agents, blocks, heavy) (csrc/mrp_config.h ENV_CFG); ids 7-10 / 11-14 are
-# MultiRobotPuzzle2 / MultiRobotPuzzleHeavy2 constructed with num_agents = 1, 3, 4, 5
+# MultiRobotPuzzle2 / MultiRobotPuzzleHeavy2 constructed with num_agents = 1, 3, 4, 5, ids 15-18 /
+# 19-22 RobotPuzzleBase(num_agents = 1, 3, 4, 5) with heavy False / True
 ENV_CFG = {0: (0, 2, 1, 0), 1: (0, 5, 1, 1), 2: (2, 2, 1, 0), 3: (2, 2, 1, 1), 4: (2, 2, 3, 1), 5: (3, 2, 1, 0), 6: (3, 2, 1, 1),
            7: (2, 1, 1, 0), 8: (2, 3, 1, 0), 9: (2, 4, 1, 0), 10: (2, 5, 1, 0),
-           11: (2, 1, 1, 1), 12: (2, 3, 1, 1), 13: (2, 4, 1, 1), 14: (2, 5, 1, 1)}
+           11: (2, 1, 1, 1), 12: (2, 3, 1, 1), 13: (2, 4, 1, 1), 14: (2, 5, 1, 1),
+           15: (3, 1, 1, 0), 16: (3, 3, 1, 0), 17: (3, 4, 1, 0), 18: (3, 5, 1, 0),
+           19: (3, 1, 1, 1), 20: (3, 3, 1, 1), 21: (3, 4, 1, 1), 22: (3, 5, 1, 1)}
 ENV_VERSION = {e: c[0] for e, c in ENV_CFG.items()}
 N_AGENTS = {e: c[1] for e, c in ENV_CFG.items()}
 N_BLOCKS = {e: c[2] for e, c in ENV_CFG.items()}
 # MultiRobotPuzzle2(num_agents=N) / MultiRobotPuzzleHeavy2(num_agents=N) -> env id
-V2_AGENT_IDS = {(h, c[1]): e for e, c in ENV_CFG.items() if c[0] == 2 and c[2] == 1 for h in (c[3],)}
+V2_AGENT_IDS = {(c[3], c[1]): e for e, c in ENV_CFG.items() if c[0] == 2 and c[2] == 1}
+# RobotPuzzleBase(num_agents=N, heavy=h) -> env id
+V3_AGENT_IDS = {(c[3], c[1]): e for e, c in ENV_CFG.items() if c[0] == 3}
 
 
 def draw_bounds(env_id: int):

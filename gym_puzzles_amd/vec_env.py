@@ -22,7 +22,7 @@ from __future__ import annotations
 import numpy as np
 
 from ._native import ENV_IDS, STATUS_FAULT, STATUS_NONFINITE, Batch, env_dims
-from .spawn import ENV_CFG, V2_AGENT_IDS
+from .spawn import ENV_CFG, V2_AGENT_IDS, V3_AGENT_IDS
 from .seeding import make_box
 
 try:   # SB3 1.x/2.x: VecEnv(num_envs, observation_space, action_space)
@@ -55,9 +55,10 @@ class MultiRobotPuzzleVecEnv(_VecEnvBase):
             # MultiRobotPuzzle2 / Heavy2(num_agents=N) (multi_robot_puzzle_02.py:139): the env id of that count
             cfg = ENV_CFG[self.env_index]
             key = (cfg[3], int(num_agents))
-            if cfg[0] != 2 or cfg[2] != 1 or key not in V2_AGENT_IDS:
+            ids = V2_AGENT_IDS if cfg[0] == 2 and cfg[2] == 1 else (V3_AGENT_IDS if cfg[0] == 3 else {})
+            if key not in ids:
                 raise NotImplementedError(f"num_agents={num_agents} is not instantiated for env {env_id!r}")
-            self.env_index = V2_AGENT_IDS[key]
+            self.env_index = ids[key]
         d = env_dims(self.env_index)
         self.num_envs = num_envs
         self.device = device

@@ -24,6 +24,8 @@
  *          6 MultiRobotPuzzle-v3 constructed with heavy=True (gym_puzzles/tests/test_env.py:12)
  *          7-10  MultiRobotPuzzle2(num_agents=1, 3, 4, 5)      (multi_robot_puzzle_02.py:139,151,354)
  *          11-14 MultiRobotPuzzleHeavy2(num_agents=1, 3, 4, 5) (multi_robot_puzzle_02.py:711)
+ *          15-18 RobotPuzzleBase(num_agents=1, 3, 4, 5)        (core.py:86-106,230)
+ *          19-22 RobotPuzzleBase(num_agents=1, 3, 4, 5, heavy=True)
  */
 #ifndef MRP_H
 #define MRP_H

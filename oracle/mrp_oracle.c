@@ -57,7 +57,7 @@ double or_rng_u01(uint64_t seed, uint64_t lane, uint64_t stream, uint64_t counte
 
 /* ---------------------------------------------------------------- configs (BASELINE.json configs) */
 typedef struct { int version, n_agents, n_blocks, heavy, obs_dim, act_dim, n_draws, max_steps; } Cfg;
-#define N_CFGS 15
+#define N_CFGS 23
 static const Cfg CFGS[N_CFGS] = {
     {0, 2, 1, 0, 28, 6, 7, 2000},   /* MultiRobotPuzzle-v0        __init__.py:3-8 */
     {0, 5, 1, 1, 40, 15, 13, 3000}, /* MultiRobotPuzzleHeavy-v0   __init__.py:10-15 */
@@ -70,6 +70,9 @@ static const Cfg CFGS[N_CFGS] = {
      * obs 9 N + 4 + 16 + 1, action 2 N, draws 1 + 2 N + 2 */
     {2, 1, 1, 0, 30, 2, 5, 2000}, {2, 3, 1, 0, 48, 6, 9, 2000}, {2, 4, 1, 0, 57, 8, 11, 2000}, {2, 5, 1, 0, 66, 10, 13, 2000},
     {2, 1, 1, 1, 30, 2, 5, 2000}, {2, 3, 1, 1, 48, 6, 9, 2000}, {2, 4, 1, 1, 57, 8, 11, 2000}, {2, 5, 1, 1, 66, 10, 13, 2000},
+    /* RobotPuzzleBase(num_agents=N[, heavy=True]), core.py:86-136: obs 4 N + 3 + 16, action 3 N, draws 3 + 2 N */
+    {3, 1, 1, 0, 23, 3, 5, 1500}, {3, 3, 1, 0, 31, 9, 9, 1500}, {3, 4, 1, 0, 35, 12, 11, 1500}, {3, 5, 1, 0, 39, 15, 13, 1500},
+    {3, 1, 1, 1, 23, 3, 5, 1500}, {3, 3, 1, 1, 31, 9, 9, 1500}, {3, 4, 1, 1, 35, 12, 11, 1500}, {3, 5, 1, 1, 39, 15, 13, 1500},
 };
 static int valid(int id) { return id >= 0 && id < N_CFGS; }
 int or_obs_dim(int id) { return valid(id) ? CFGS[id].obs_dim : -1; }

@@ -31,9 +31,12 @@ ENV_IDS = {
     "MultiRobotPuzzle-v2-agents1": 7, "MultiRobotPuzzle-v2-agents3": 8, "MultiRobotPuzzle-v2-agents4": 9,
     "MultiRobotPuzzle-v2-agents5": 10, "MultiRobotPuzzleHeavy-v2-agents1": 11, "MultiRobotPuzzleHeavy-v2-agents3": 12,
     "MultiRobotPuzzleHeavy-v2-agents4": 13, "MultiRobotPuzzleHeavy-v2-agents5": 14,
+    "MultiRobotPuzzle-v3-agents1": 15, "MultiRobotPuzzle-v3-agents3": 16, "MultiRobotPuzzle-v3-agents4": 17,
+    "MultiRobotPuzzle-v3-agents5": 18, "MultiRobotPuzzle-v3-heavy-agents1": 19, "MultiRobotPuzzle-v3-heavy-agents3": 20,
+    "MultiRobotPuzzle-v3-heavy-agents4": 21, "MultiRobotPuzzle-v3-heavy-agents5": 22,
 }
 # env id -> 0 (multi_robot_puzzle_00.py), 2 (multi_robot_puzzle_02.py), 3 (core.py)
-ENV_VERSION = {0: 0, 1: 0, 2: 2, 3: 2, 4: 2, 5: 3, 6: 3, **{e: 2 for e in range(7, 15)}}
+ENV_VERSION = {0: 0, 1: 0, 2: 2, 3: 2, 4: 2, 5: 3, 6: 3, **{e: 2 for e in range(7, 15)}, **{e: 3 for e in range(15, 23)}}
 
 
 def build() -> str:

@@ -9,7 +9,10 @@ DIMS = {0: (2, 1, 8, 21), 1: (5, 1, 11, 48), 2: (2, 1, 12, 53), 3: (2, 1, 12, 53
         5: (2, 1, 8, 21), 6: (2, 1, 8, 21),
         # MultiRobotPuzzle2 / Heavy2 with num_agents = 1, 3, 4, 5 (DimsV2<N>)
         7: (1, 1, 9, 26), 8: (3, 1, 15, 89), 9: (4, 1, 18, 134), 10: (5, 1, 21, 188),
-        11: (1, 1, 9, 26), 12: (3, 1, 15, 89), 13: (4, 1, 18, 134), 14: (5, 1, 21, 188)}
+        11: (1, 1, 9, 26), 12: (3, 1, 15, 89), 13: (4, 1, 18, 134), 14: (5, 1, 21, 188),
+        # RobotPuzzleBase(num_agents = 1, 3, 4, 5[, heavy=True]) (DimsV3<N>)
+        15: (1, 1, 7, 14), 16: (3, 1, 9, 29), 17: (4, 1, 10, 38), 18: (5, 1, 11, 48),
+        19: (1, 1, 7, 14), 20: (3, 1, 9, 29), 21: (4, 1, 10, 38), 22: (5, 1, 11, 48)}
 
 
 def tree_n(nf: int) -> int:

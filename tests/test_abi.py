@@ -53,7 +53,10 @@ def test_python_binding_lists_every_symbol(lib):
     (6, (27, 6, 7, 2, 1, 1500)),
     # MultiRobotPuzzle2 / Heavy2(num_agents=N): obs 9 N + 21, action 2 N, draws 2 N + 3 (_02.py:178-194)
     (7, (30, 2, 5, 1, 1, 2000)), (8, (48, 6, 9, 3, 1, 2000)), (9, (57, 8, 11, 4, 1, 2000)), (10, (66, 10, 13, 5, 1, 2000)),
-    (11, (30, 2, 5, 1, 1, 2000)), (12, (48, 6, 9, 3, 1, 2000)), (13, (57, 8, 11, 4, 1, 2000)), (14, (66, 10, 13, 5, 1, 2000))])
+    (11, (30, 2, 5, 1, 1, 2000)), (12, (48, 6, 9, 3, 1, 2000)), (13, (57, 8, 11, 4, 1, 2000)), (14, (66, 10, 13, 5, 1, 2000)),
+    # RobotPuzzleBase(num_agents=N[, heavy]): obs 4 N + 19, action 3 N, draws 2 N + 3 (core.py:121-136)
+    (15, (23, 3, 5, 1, 1, 1500)), (16, (31, 9, 9, 3, 1, 1500)), (17, (35, 12, 11, 4, 1, 1500)), (18, (39, 15, 13, 5, 1, 1500)),
+    (19, (23, 3, 5, 1, 1, 1500)), (20, (31, 9, 9, 3, 1, 1500)), (21, (35, 12, 11, 4, 1, 1500)), (22, (39, 15, 13, 5, 1, 1500))])
 def test_env_dims(lib, env_id, dims):
     from gym_puzzles_amd import env_dims
     d = env_dims(env_id)
@@ -62,7 +65,7 @@ def test_env_dims(lib, env_id, dims):
 
 def test_env_dims_match_oracle(lib, oracle_lib):
     from gym_puzzles_amd import env_dims
-    for e in range(15):
+    for e in range(23):
         d = env_dims(e)
         assert d["n_agents"] == oracle_lib.or_n_agents(e) and d["n_blocks"] == oracle_lib.or_n_blocks(e)
         assert d["obs_dim"] == oracle_lib.or_obs_dim(e) and d["act_dim"] == oracle_lib.or_act_dim(e)
@@ -72,17 +75,18 @@ def test_env_dims_match_oracle(lib, oracle_lib):
 def test_bad_env_id(lib):
     from gym_puzzles_amd import env_dims
     with pytest.raises(ValueError):
-        env_dims(15)
+        env_dims(23)
     h = ctypes.c_void_p()
-    assert lib.mrp_create(15, 4, 0, 0, 0, ctypes.byref(h)) == -1
+    assert lib.mrp_create(23, 4, 0, 0, 0, ctypes.byref(h)) == -1
     assert b"env_id" in lib.mrp_last_error(None)
 
 
 def test_state_words_positive(lib):
-    w = [lib.mrp_state_words(e) for e in range(15)]
+    w = [lib.mrp_state_words(e) for e in range(23)]
     assert all(x > 0 for x in w) and w[1] > w[0] and w[4] > w[2] and w[5] == w[6] == w[0]
     assert w[7] < w[2] < w[8] < w[9] < w[10] and w[7:11] == w[11:15]
-    assert lib.mrp_state_words(15) < 0
+    assert w[15] < w[5] < w[16] < w[17] < w[18] and w[15:19] == w[19:23]
+    assert lib.mrp_state_words(23) < 0
 
 
 def test_no_cpu_fallback_without_device(lib):
@@ -108,7 +112,7 @@ def test_lane_layout_restatement_matches_library(lib):
     """tests/lane_layout.py (the LaneState word offsets the fault-injection GPU tests write
     through mrp_set_state) sizes every env's lane exactly as the library does."""
     from lane_layout import offsets
-    for e in range(15):
+    for e in range(23):
         off, words = offsets(e)
         assert words == lib.mrp_state_words(e), e
         assert off["nonfinite"] + 2 <= words and off["fault"] < off["agent_dist"]

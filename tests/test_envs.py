@@ -184,6 +184,12 @@ def test_num_agents_maps_to_its_env_id():
             cls(num_agents=0)
     with pytest.raises(NotImplementedError):
         envs.MultiRobotPuzzleHeavy2ThreeBlock(num_agents=3)
+    from gym_puzzles_amd.spawn import V3_AGENT_IDS
+    for heavy in (0, 1):
+        for n in range(1, 6):
+            assert ENV_CFG[V3_AGENT_IDS[(heavy, n)]] == (3, n, 1, heavy)
+    with pytest.raises(NotImplementedError):
+        envs.RobotPuzzleBase(num_agents=6)
 
 
 @pytest.mark.gpu
@@ -208,6 +214,33 @@ def test_multi_robot_puzzle2_num_agents(gpu_lib, heavy, n):
     rs = np.random.RandomState(5 + n)
     for _ in range(40):
         a = rs.uniform(-1, 1, 2 * n).astype(np.float32)
+        ob, r, d, _ = env.step(a)
+        mo, _, md, _ = mirror.step(a[None])
+        assert np.array_equal(ob.astype(np.float32), mo[0]) and r == mirror.reward64[0] and d == bool(md[0])
+        if d:
+            break
+    mirror.close()
+    env.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("heavy", [False, True])
+@pytest.mark.parametrize("n", [1, 3, 5])
+def test_robot_puzzle_base_num_agents(gpu_lib, heavy, n):
+    """RobotPuzzleBase(num_agents=N, heavy=h): spaces of core.py:121-136 (4 obs per agent in
+    [-2.5, 2.5] x2, [-2pi, 2pi], [0, 1]; block 3; 16 vertices in [-1.5, 1.5]; 3 action values per
+    agent), steps equal to its env id's batch given the same state."""
+    from gym_puzzles_amd import Batch, RobotPuzzleBase
+    env = RobotPuzzleBase(num_agents=n, heavy=heavy)
+    assert env.num_agents == n and env.observation_space.shape == (4 * n + 19,) and env.action_space.shape == (3 * n,)
+    assert env.observation_space.low[3] == 0.0 and env.observation_space.high[4 * n + 2] == np.float32(2 * np.pi)
+    mirror = Batch(env.env_id, 1)
+    mirror.set_time_limit(0)
+    mirror.set_reward_params(10, 0.1, 50, 0.025, 100)
+    mirror.set_state(env._b.get_state())
+    rs = np.random.RandomState(11 + n)
+    for _ in range(40):
+        a = rs.uniform(-1, 1, 3 * n).astype(np.float32)
         ob, r, d, _ = env.step(a)
         mo, _, md, _ = mirror.step(a[None])
         assert np.array_equal(ob.astype(np.float32), mo[0]) and r == mirror.reward64[0] and d == bool(md[0])

@@ -18,8 +18,9 @@ from gym_puzzles_amd.spawn import draw_bounds, reference_draws
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 ENVS = range(7)
-# MultiRobotPuzzle2 / MultiRobotPuzzleHeavy2(num_agents = 1, 3, 4, 5) (multi_robot_puzzle_02.py:139)
-AGENT_VARIANTS = range(7, 15)
+# MultiRobotPuzzle2 / MultiRobotPuzzleHeavy2(num_agents = 1, 3, 4, 5) (multi_robot_puzzle_02.py:139) and
+# RobotPuzzleBase(num_agents = 1, 3, 4, 5[, heavy=True]) (core.py:88)
+AGENT_VARIANTS = range(7, 23)
 
 
 @pytest.fixture(scope="module")

@@ -65,11 +65,11 @@ AGENT_V2 = [(-0.039, -0.095), (0.039, -0.095), (0.095, -0.039), (0.095, 0.039), 
 
 
 def _expected_masses(env_id):
-    if env_id in (5, 6):   # Block("T") blocks.py:80-90 at scale 0.5 / 1, density 5 / 10; Robot robot.py:34-40
-        s, dens = (1.0, 10.0) if env_id == 6 else (0.5, 5.0)
+    if ENV_CFG[env_id][0] == 3:   # Block("T") blocks.py:80-90 at scale 0.5 / 1, density 5 / 10; Robot robot.py:34-40
+        s, dens = (1.0, 10.0) if ENV_CFG[env_id][3] else (0.5, 5.0)
         blk = _compound([_poly_mass(_box(1 * s, 1 * s, 0, -1 * s), dens), _poly_mass(_box(3 * s, 1 * s, 0, 1 * s), dens)])
         agent = _poly_mass([(x * 8.0, y * 8.0) for x, y in AGENT_V2], 5.0)
-        return [blk, agent, agent]
+        return [blk] + [agent] * ENV_CFG[env_id][1]
     if env_id in (0, 1):
         s = 2.0 if env_id == 1 else 1.0
         blk = _compound([_poly_mass(_box(0.5 * s, 0.5 * s, 0, -0.5 * s), 5.0 * (2 if env_id == 1 else 1)),
@@ -87,7 +87,7 @@ def _expected_masses(env_id):
     return [t, l_blk, i_blk, agent, agent]
 
 
-@pytest.mark.parametrize("env_id", range(15))
+@pytest.mark.parametrize("env_id", range(23))
 def test_mass_known_answers(orc, env_id):
     e = orc.OracleEnv(env_id)
     e.reset(reference_draws(env_id, np.random.RandomState(17)), np.zeros(e.act_dim, np.float32))
@@ -196,38 +196,39 @@ def _t_vertices_v3(s):
     return np.array(wide + stem, np.float64)
 
 
-@pytest.mark.parametrize("env_id", [5, 6])
+@pytest.mark.parametrize("env_id", [5, 6, 15, 18, 19, 22])
 def test_v3_obs_and_reward_restatement(orc, env_id):
     """Recompute the v3 observation and reward in numpy from the oracle's bodies: normalised
     poses (x - ws) / ws, (y - hs) / ws, angle % 2 pi; the goal (5/6 * 640 - 4/3, 240) px; eight
-    normalised T vertices; reward weights 50 / 0.025 / 10 / 0.1 with the agent terms over 4."""
+    normalised T vertices; reward weights 50 / 0.025 / 10 / 0.1 with the agent terms over 4; any num_agents (core.py:88)."""
     ws, hs = 640 / 30 / 2, 480 / 30 / 2
     gx, gy = (5 / 6 * 640 - 4 / 3 - 320) / 320, (240 - 240) / 320
-    s = 1.0 if env_id == 6 else 0.5
+    s = 1.0 if ENV_CFG[env_id][3] else 0.5
+    na = ENV_CFG[env_id][1]
     e = orc.OracleEnv(env_id)
     rs = np.random.RandomState(8)
-    obs = e.reset(reference_draws(env_id, rs), rs.uniform(-1, 1, 6).astype(np.float32))
+    obs = e.reset(reference_draws(env_id, rs), rs.uniform(-1, 1, 3 * na).astype(np.float32))
     verts = _t_vertices_v3(s)
     lcy = e.body_mass(0)[3]
 
     def poses(b):
         n = lambda x, y: ((x - ws) / ws, (y - hs) / ws)
-        return n(*b[0, :2].astype(np.float64)), [n(*b[1 + i, :2].astype(np.float64)) for i in range(2)]
+        return n(*b[0, :2].astype(np.float64)), [n(*b[1 + i, :2].astype(np.float64)) for i in range(na)]
 
     def dists(b):
         (bx, by), ag = poses(b)
         return math.hypot(bx - gx, by - gy), [math.hypot(ax - bx, ay - by) for ax, ay in ag]
 
-    prev_bd, prev_ad = dists(e.bodies().reshape(3, 6))
+    prev_bd, prev_ad = dists(e.bodies().reshape(1 + na, 6))
     for t in range(60):
-        a = rs.uniform(-1, 1, 6).astype(np.float32)
+        a = rs.uniform(-1, 1, 3 * na).astype(np.float32)
         obs, rew, done, _ = e.step(a)
-        b = e.bodies().reshape(3, 6)
+        b = e.bodies().reshape(1 + na, 6)
         (bx, by), ag = poses(b)
         bd, ad = dists(b)
         brot = float(b[0, 2]) % (2 * np.pi)
         exp = []
-        for i in range(2):
+        for i in range(na):
             exp += [bx - ag[i][0], by - ag[i][1], float(b[1 + i, 2]) % (2 * np.pi), 0.0]
         exp += [gx - bx, gy - by, 0.0 - brot]
         ca, sa = math.cos(b[0, 2]), math.sin(b[0, 2])
@@ -236,13 +237,13 @@ def test_v3_obs_and_reward_restatement(orc, env_id):
             exp += [(ox + ca * vx - sa * vy - ws) / ws, (oy + sa * vx + ca * vy - hs) / ws]
         np.testing.assert_allclose(obs, exp, rtol=1e-5, atol=2e-5)
         r = (prev_bd - bd) * 50 - 0.025 * bd
-        for i in range(2):
+        for i in range(na):
             r += (prev_ad[i] - ad[i]) * 10 / 4. - 0.1 * ad[i] / 4.
         if bd <= 25 / 640 * 2:
             r += 100
         assert rew == pytest.approx(r, rel=1e-5, abs=1e-5)
         assert bool(done) == (bd <= 25 / 640 * 2)
-        assert e.flags()[0].tolist() == [0, 0]   # the v3 contact detector never fires
+        assert e.flags()[0].tolist() == [0] * na   # the v3 contact detector never fires
         prev_bd, prev_ad = bd, ad
 
 
@@ -363,7 +364,7 @@ def _pools():
 POOLS = _pools()
 
 
-@pytest.mark.parametrize("env_id", range(15))
+@pytest.mark.parametrize("env_id", range(23))
 def test_device_pools_hold_the_oracle_high_water_marks(oracle_lib, env_id):
     from gym_puzzles_amd.spawn import draw_bounds
     from oracle.oracle import batch_capacity
@@ -374,7 +375,7 @@ def test_device_pools_hold_the_oracle_high_water_marks(oracle_lib, env_id):
     assert caps["move_buffer"] >= 1 and caps["contacts"] >= 1
 
 
-@pytest.mark.parametrize("env_id", range(15))
+@pytest.mark.parametrize("env_id", range(23))
 def test_oracle_under_asan_ubsan(env_id):
     """The oracle's sources built with AddressSanitizer + UBSan (make -C oracle asan, every finding
     fatal) run the synthetic workload of every env id cleanly: 64 lanes x 500 steps, TimeLimit 60

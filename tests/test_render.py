@@ -13,7 +13,7 @@ import pytest
 from gym_puzzles_amd.spawn import ENV_VERSION
 from oracle import render_ref
 
-ENVS = list(range(7)) + [7, 10, 14]   # num_agents variants 1 and 5 (light / heavy)
+ENVS = list(range(7)) + [7, 10, 14, 15, 18, 22]   # num_agents variants 1 and 5 (light / heavy)
 
 
 def _dims(env_id):
