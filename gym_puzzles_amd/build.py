@@ -44,14 +44,30 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(d) <= t for d in DEPS if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=(), jobs: int | None = None) -> str:
-    """Build libmrp.so (or a diagnostic variant with extra -D defines into ``out``)."""
+def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=(), jobs: int | None = None,
+          only_envs=None) -> str:
+    """Build libmrp.so (or a diagnostic variant with extra -D defines into ``out``).
+
+    ``only_envs`` (A/B libraries): compile only those env units (plus the small shared units) and link
+    the other env units' objects of the default build, which must exist; each env unit is
+    self-contained, so the variant differs from the default library only in the listed envs."""
     if not force and out == OUT and up_to_date():
         return out
     objdir = os.path.join(HERE, "build", os.path.basename(out) + ".obj")
     os.makedirs(objdir, exist_ok=True)
     dflags = [f"-D{d}" for d in defines]
     objs = [os.path.join(objdir, os.path.basename(s) + ".o") for s in SOURCES]
+    todo = list(range(len(SOURCES)))
+    if only_envs is not None:
+        assert out != OUT, "only_envs builds a variant library, never the default one"
+        keep = {f"mrp_env{e}.hip" for e in only_envs}
+        base = os.path.join(HERE, "build", os.path.basename(OUT) + ".obj")
+        todo = [i for i, s in enumerate(SOURCES) if "mrp_env" not in s or os.path.basename(s) in keep]
+        for i, s in enumerate(SOURCES):
+            if i not in todo:
+                objs[i] = os.path.join(base, os.path.basename(s) + ".o")
+                if not os.path.exists(objs[i]):
+                    raise FileNotFoundError(f"{objs[i]}: build the default library first")
 
     def compile_one(i: int) -> None:
         cmd = [hipcc()] + FLAGS + dflags + ["-c", SOURCES[i], "-o", objs[i]]
@@ -61,7 +77,7 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
 
     # slowest units first; each hipcc is single-threaded, so one job per core
     jobs = jobs or max(1, min(len(SOURCES), os.cpu_count() or 1, int(os.environ.get("MAX_JOBS", "16"))))
-    order = sorted(range(len(SOURCES)), key=lambda i: "mrp_env" not in SOURCES[i])
+    order = sorted(todo, key=lambda i: "mrp_env" not in SOURCES[i])
     with ThreadPoolExecutor(jobs) as ex:
         list(ex.map(compile_one, order))
     cmd = [hipcc()] + FLAGS + ["-shared"] + objs + ["-o", out + ".tmp"]
@@ -77,5 +93,11 @@ if __name__ == "__main__":
         print(build(force=True, verbose=True, out=os.path.join(HERE, "libmrp_stamps.so"), defines=("MRP_STAMPS",)))
     elif "--progress" in sys.argv:   # diagnostic hang-localisation build (tools/hang_probe.py)
         print(build(force=True, verbose=True, out=os.path.join(HERE, "libmrp_progress.so"), defines=("MRP_PROGRESS",)))
+    elif "--variant" in sys.argv:   # A/B library: python -m gym_puzzles_amd.build --variant OUT.so E [E ...] [-DNAME ...]
+        i = sys.argv.index("--variant")
+        args = sys.argv[i + 2:]
+        envs = [int(a) for a in args if not a.startswith("-D")]
+        defs = [a[2:] for a in args if a.startswith("-D")]
+        print(build(force=True, verbose=True, out=os.path.abspath(sys.argv[i + 1]), defines=defs, only_envs=envs))
     else:
         print(build(force="--force" in sys.argv, verbose=True))
