@@ -1034,7 +1034,71 @@ template <int ENV> struct World {
     // whenever k and iters have the same parity.  The state is compared at the k with
     // iters - k = 0 mod 4 against a snapshot taken two sweeps earlier (every fourth sweep rather
     // than every second: the comparison is off the sweeps' dependency chain but not free).
+#ifndef MRP_SCHED_WIDE_AGENTS
+#define MRP_SCHED_WIDE_AGENTS 99
+#endif
+    // envs whose islands reach 5-8 contacts get scheduled sweeps for those too (more code per kernel)
+    static constexpr bool SCHED_WIDE = NB > 1 || NA >= MRP_SCHED_WIDE_AGENTS;
+    // islands of NC = 3 or 4 contacts (the slowest lanes' islands): the contacts' bodies and point
+    // counts are read out of their lanes once, before the sweeps, into scalar registers, and the
+    // contact loop is unrolled, so a contact update issues no readlane for its schedule and the body
+    // readlanes take a lane select written long before (no wait states); same operations and order as
+    // the generic loop below
+    template <int NC>
+    __device__ __forceinline__ int lanes_sweeps(Isl& is, VC* vcs, int iters, bool early_exit) {
+        const int me = tid < NC ? tid : 0;
+        CC my = load_cc(vcs[me]);
+        const int cia = vcs[me].iaI, cib = vcs[me].ibI;
+        const int bk = tid < is.nb ? tid : 0;
+        float bvx = is.vvx[bk], bvy = is.vvy[bk], bw = is.vw[bk];
+        int ia[NC], ib[NC], pc[NC];
+#pragma unroll
+        for (int i = 0; i < NC; ++i) { ia[i] = rdli(cia, i); ib[i] = rdli(cib, i); pc[i] = rdli(my.pcount, i); }
+        P2 sni = my.ni, sti = my.ti;
+        float sbx = bvx, sby = bvy, sbw = bw;
+        bool have = snap_initial(iters);
+        int sweeps = 0;
+        for (int it = 0; it < iters; ++it) {
+            ++sweeps;
+#pragma unroll
+            for (int i = 0; i < NC; ++i) {
+                P2 vA = p2(rdl(bvx, ia[i]), rdl(bvy, ia[i])); float wA = rdl(bw, ia[i]);
+                P2 vB = p2(rdl(bvx, ib[i]), rdl(bvy, ib[i])); float wB = rdl(bw, ib[i]);
+                P2 ni, ti;
+                vel_update(my, pc[i], [i](bool x) { return lane_bit(x, i); }, ni, ti, vA, wA, vB, wB);
+                if (tid == i) { my.ni = ni; my.ti = ti; }
+                bvx = wrl(bvx, rdl(vA.x, i), ia[i]); bvy = wrl(bvy, rdl(vA.y, i), ia[i]); bw = wrl(bw, rdl(wA, i), ia[i]);
+                bvx = wrl(bvx, rdl(vB.x, i), ib[i]); bvy = wrl(bvy, rdl(vB.y, i), ib[i]); bw = wrl(bw, rdl(wB, i), ib[i]);
+            }
+            const int left = iters - (it + 1);
+            if (early_exit && (left & 3) == 0 && have) {
+                const uint32_t d = (__float_as_uint(my.ni.x) ^ __float_as_uint(sni.x)) | (__float_as_uint(my.ni.y) ^ __float_as_uint(sni.y)) |
+                                   (__float_as_uint(my.ti.x) ^ __float_as_uint(sti.x)) | (__float_as_uint(my.ti.y) ^ __float_as_uint(sti.y)) |
+                                   (__float_as_uint(bvx) ^ __float_as_uint(sbx)) | (__float_as_uint(bvy) ^ __float_as_uint(sby)) |
+                                   (__float_as_uint(bw) ^ __float_as_uint(sbw));
+                if (__builtin_amdgcn_ballot_w64(d != 0u) == 0) break;
+            }
+            if (early_exit && (left & 3) == 2) {
+                sni = my.ni; sti = my.ti; sbx = bvx; sby = bvy; sbw = bw;
+                have = true;
+            }
+        }
+        if (tid < is.nb) { is.vvx[tid] = bvx; is.vvy[tid] = bvy; is.vw[tid] = bw; }
+        if (tid < NC) store_cc(vcs[tid], my);
+        return sweeps;
+    }
     __device__ __forceinline__ int solver_velocity_lanes(Isl& is, VC* vcs, int iters, bool early_exit = true) {
+        {
+            const int n = __builtin_amdgcn_readfirstlane(is.nc);
+            if (n == 3) return lanes_sweeps<3>(is, vcs, iters, early_exit);
+            if (n == 4) return lanes_sweeps<4>(is, vcs, iters, early_exit);
+            if constexpr (SCHED_WIDE) {   // islands of 5-8 contacts (the 3-block config: +4 %)
+                if (n == 5) return lanes_sweeps<5>(is, vcs, iters, early_exit);
+                if (n == 6) return lanes_sweeps<6>(is, vcs, iters, early_exit);
+                if (n == 7) return lanes_sweeps<7>(is, vcs, iters, early_exit);
+                if (n == 8) return lanes_sweeps<8>(is, vcs, iters, early_exit);
+            }
+        }
         const int nc = is.nc;
         CC my = load_cc(vcs[tid < nc ? tid : 0]);   // lanes >= nc evaluate a copy of contact 0 and are never kept
         const int cia = vcs[tid < nc ? tid : 0].iaI, cib = vcs[tid < nc ? tid : 0].ibI;
@@ -1376,14 +1440,19 @@ template <int ENV> struct World {
     // Rotations as packed (c, s) pairs: pmul_rv(q, v) = q * v.x + pperp(q) * v.y (see P2).
     __device__ __forceinline__ static P2 rot_cs(float angle) { const Rot q = rot(angle); return p2(q.c, q.s); }
     __device__ __forceinline__ static P2 prot(P2 q, P2 v) { return q * pbc(v.x) + pperp(q) * pbc(v.y); }
+    // Rotation memo of the position passes: an angle of +0 (a static body's island angle) is answered
+    // directly, other angles from two entries keyed by the bit pattern, the least recently used one
+    // replaced on a miss (an agent with invI = 0 keeps its entry while the block's angle changes at
+    // every point: 3 b2Rot::Set per pass fewer than round-robin on a 3-contact agent-block-wall island)
     struct RotMemo {
-        uint32_t k0 = 0u, k1 = 0u;   // +0.0f: b2Rot::Set(+0) = {+0, 1}
+        uint32_t k0 = 0u, k1 = 0u;
         P2 q0 = {1.0f, 0.0f}, q1 = {1.0f, 0.0f};
         bool next1 = false;
         __device__ __forceinline__ P2 get(float angle) {
             const uint32_t b = __float_as_uint(angle);
-            if (b == k0) return q0;
-            if (b == k1) return q1;
+            if (b == 0u) return p2(1.0f, 0.0f);   // +0 (every static body's island angle): b2Rot::Set(+0) = {s +0, c 1}
+            if (b == k0) { next1 = true; return q0; }   // least recently used entry is replaced
+            if (b == k1) { next1 = false; return q1; }
             const P2 q = rot_cs(angle);
             if (next1) { k1 = b; q1 = q; } else { k0 = b; q0 = q; }
             next1 = !next1;
@@ -1400,8 +1469,9 @@ template <int ENV> struct World {
         bool next1 = false;
         __device__ __forceinline__ P2 get(float angle) {
             const uint32_t b = __float_as_uint(angle);
-            if (uni(b == k0)) return q0;
-            if (uni(b == k1)) return q1;
+            if (uni(b == 0u)) return p2(1.0f, 0.0f);
+            if (uni(b == k0)) { next1 = true; return q0; }
+            if (uni(b == k1)) { next1 = false; return q1; }
             const P2 q = rot_cs(angle);
             if (next1) { k1 = b; q1 = q; } else { k0 = b; q0 = q; }
             next1 = !next1;
@@ -1483,8 +1553,11 @@ template <int ENV> struct World {
     template <int NC, bool SAMEB, bool XA0, bool XA1>
     __device__ __forceinline__ int pos_sweep(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB, int iters,
                                              int p, int q, int z) {
-        const PCC c0 = load_pcc(vcs[0], pcs[0], toi, toiA, toiB);
-        const PCC c1 = load_pcc(vcs[NC - 1], pcs[NC - 1], toi, toiA, toiB);
+        PCC c0 = load_pcc(vcs[0], pcs[0], toi, toiA, toiB);
+        PCC c1 = load_pcc(vcs[NC - 1], pcs[NC - 1], toi, toiA, toiB);
+        // point counts and manifold types are wave-uniform: read into scalar registers once, not per pass
+        c0.pcount = __builtin_amdgcn_readfirstlane(c0.pcount); c0.type = __builtin_amdgcn_readfirstlane(c0.type);
+        c1.pcount = __builtin_amdgcn_readfirstlane(c1.pcount); c1.type = __builtin_amdgcn_readfirstlane(c1.type);
         P2 cP = p2(is.pcx[p], is.pcy[p]), cQ = p2(is.pcx[q], is.pcy[q]), cZ = p2(is.pcx[z], is.pcy[z]);
         float aP = is.pa[p], aQ = is.pa[q], aZ = is.pa[z];
         const float baum = toi ? TOI_BAUMGARTE : BAUMGARTE;
@@ -1527,7 +1600,48 @@ template <int ENV> struct World {
         return -1;
     }
 
+    // position passes of islands of NC = 3 or 4 contacts with the schedule (bodies, point counts,
+    // manifold types) read out of the lanes once, before the passes (see lanes_sweeps)
+    template <int NC>
+    __device__ __forceinline__ int lanes_passes(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB, int iters) {
+        const int me = tid < NC ? tid : 0;
+        const PCC my = load_pcc(vcs[me], pcs[me], toi, toiA, toiB);
+        const int cia = vcs[me].iaI, cib = vcs[me].ibI;
+        const int bk = tid < is.nb ? tid : 0;
+        float bx = is.pcx[bk], by = is.pcy[bk], ba = is.pa[bk];
+        const float baum = toi ? TOI_BAUMGARTE : BAUMGARTE;
+        const float exitSep = toi ? -1.5f * LINEAR_SLOP : -3.0f * LINEAR_SLOP;
+        int ia[NC], ib[NC], pc[NC], ty[NC];
+#pragma unroll
+        for (int i = 0; i < NC; ++i) { ia[i] = rdli(cia, i); ib[i] = rdli(cib, i); pc[i] = rdli(my.pcount, i); ty[i] = rdli(my.type, i); }
+        RotMemo memo;
+        int it = 0;
+        while (it < iters) {
+            ++it;
+            float minSep = 0.0f;
+#pragma unroll
+            for (int i = 0; i < NC; ++i) {
+                P2 cA = p2(rdl(bx, ia[i]), rdl(by, ia[i])); float aA = rdl(ba, ia[i]);
+                P2 cB = p2(rdl(bx, ib[i]), rdl(by, ib[i])); float aB = rdl(ba, ib[i]);
+                auto get = [&memo, i](float a) { return memo.get(rdl(a, i)); };
+                pos_update(my, pc[i], ty[i], baum, get, get, [&minSep, i](float sep) { minSep = fmin_(minSep, rdl(sep, i)); },
+                           cA, aA, cB, aB);
+                bx = wrl(bx, rdl(cA.x, i), ia[i]); by = wrl(by, rdl(cA.y, i), ia[i]); ba = wrl(ba, rdl(aA, i), ia[i]);
+                bx = wrl(bx, rdl(cB.x, i), ib[i]); by = wrl(by, rdl(cB.y, i), ib[i]); ba = wrl(ba, rdl(aB, i), ib[i]);
+            }
+            if (minSep >= exitSep) break;
+        }
+        if (tid < is.nb) { is.pcx[tid] = bx; is.pcy[tid] = by; is.pa[tid] = ba; }
+        return it;
+    }
     __device__ __forceinline__ int solver_position_lanes(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB, int iters) {
+        // single-block envs only: in the 3-block config the scheduled passes measured slower (-2.7 %,
+        // also with 5-8 contact islands scheduled; profiles/r3g_ab_env4_schedules.txt)
+        if constexpr (NB == 1) {
+            const int n = __builtin_amdgcn_readfirstlane(is.nc);
+            if (n == 3) return lanes_passes<3>(is, vcs, pcs, toi, toiA, toiB, iters);
+            if (n == 4) return lanes_passes<4>(is, vcs, pcs, toi, toiA, toiB, iters);
+        }
         const int nc = is.nc;
         const int me = tid < nc ? tid : 0;   // lanes >= nc evaluate a copy of contact 0 and are never kept
         const PCC my = load_pcc(vcs[me], pcs[me], toi, toiA, toiB);
