@@ -1035,9 +1035,9 @@ template <int ENV> struct World {
     // iters - k = 0 mod 4 against a snapshot taken two sweeps earlier (every fourth sweep rather
     // than every second: the comparison is off the sweeps' dependency chain but not free).
 #ifndef MRP_SCHED_WIDE_AGENTS
-#define MRP_SCHED_WIDE_AGENTS 99
+#define MRP_SCHED_WIDE_AGENTS 5   // Heavy-v0 (5 agents): +5.9 % in the driver window (profiles/r3g_ab_envs_1_2_5.txt)
 #endif
-    // envs whose islands reach 5-8 contacts get scheduled sweeps for those too (more code per kernel)
+    // envs whose islands reach 5-8 contacts (several blocks, or 5 agents) get scheduled sweeps for those too
     static constexpr bool SCHED_WIDE = NB > 1 || NA >= MRP_SCHED_WIDE_AGENTS;
     // islands of NC = 3 or 4 contacts (the slowest lanes' islands): the contacts' bodies and point
     // counts are read out of their lanes once, before the sweeps, into scalar registers, and the
