@@ -22,7 +22,14 @@ SOURCES = ([os.path.join(CSRC, "mrp_kernels.hip"), os.path.join(CSRC, "mrp_table
            + [os.path.join(CSRC, f"mrp_env{e}.hip") for e in range(N_ENVS)])
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("mrp_math.h", "mrp_config.h", "mrp_world.h", "mrp_env.h", "mrp_tables.h",
                                                   "mrp_ops.h", "mrp_lane.h", "mrp_render.h")] + [
-    os.path.join(HERE, "..", "include", "mrp.h")]
+    os.path.join(HERE, "..", "include", "mrp.h"), os.path.abspath(__file__)]
+# Per-unit flags.  The 3-block config (env 4, islands of 5-8 contacts) keeps its lanes-path sweep /
+# pass loops as functions of their own, scheduled for ILP: the machine scheduler then drops the
+# lanes-path update's s_nop wait states from about 40 to 17, +5.7 % env-steps/s in the driver window
+# and +6.6 % at steps 21-220 (A/B, profiles/r3g_ab_scheduler.txt).  For v0 the same build gives
+# +1.5 % in the driver window but -2.7 % at steps 21-220 (a call per island solve), so v0 keeps the
+# inlined form.
+UNIT_FLAGS = {"mrp_env4.hip": ["-DMRP_SOLVE_NOINLINE_LANES", "-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
 # -fno-slp-vectorize: the serial solver chains are latency-bound; packing pairs of f32 ops into
 # v_pk_* costs operand-shuffling moves on the dependency chain (measured +2-3 % env-steps/s off)
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
@@ -69,8 +76,12 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
                 if not os.path.exists(objs[i]):
                     raise FileNotFoundError(f"{objs[i]}: build the default library first")
 
+    # A/B only: extra compiler flags for a variant library (never the default one)
+    extra = os.environ.get("MRP_EXTRA_FLAGS", "").split() if out != OUT else []
+
     def compile_one(i: int) -> None:
-        cmd = [hipcc()] + FLAGS + dflags + ["-c", SOURCES[i], "-o", objs[i]]
+        unit = UNIT_FLAGS.get(os.path.basename(SOURCES[i]), []) if not extra else []
+        cmd = [hipcc()] + FLAGS + unit + extra + dflags + ["-c", SOURCES[i], "-o", objs[i]]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

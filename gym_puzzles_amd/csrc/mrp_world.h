@@ -26,6 +26,19 @@ namespace mrp {
 
 constexpr int NULLN = -1;
 
+// The solver's sweep / pass loops (one call per island solve).  MRP_SOLVE_NOINLINE (A/B) keeps each
+// as a function of its own, so the machine scheduler treats its loop as it does in a small kernel.
+#ifdef MRP_SOLVE_NOINLINE
+#define MRP_SOLVE_FN __device__ __attribute__((noinline))
+#else
+#define MRP_SOLVE_FN __device__ __forceinline__
+#endif
+#ifdef MRP_SOLVE_NOINLINE_LANES
+#define MRP_LANES_FN __device__ __attribute__((noinline))
+#else
+#define MRP_LANES_FN MRP_SOLVE_FN
+#endif
+
 // v_writelane_b32 (clang exposes no builtin for it; the LLVM intrinsic is bound by name, so the
 // compiler still inserts the readlane -> writelane wait states itself)
 extern "C" __device__ int mrp_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
@@ -1045,7 +1058,7 @@ template <int ENV> struct World {
     // readlanes take a lane select written long before (no wait states); same operations and order as
     // the generic loop below
     template <int NC>
-    __device__ __forceinline__ int lanes_sweeps(Isl& is, VC* vcs, int iters, bool early_exit) {
+    MRP_LANES_FN int lanes_sweeps(Isl& is, VC* vcs, int iters, bool early_exit) {
         const int me = tid < NC ? tid : 0;
         CC my = load_cc(vcs[me]);
         const int cia = vcs[me].iaI, cib = vcs[me].ibI;
@@ -1328,7 +1341,7 @@ template <int ENV> struct World {
                                                                        : sweep_one<1>(is, vcs, iters, early_exit);
     }
     template <int P0>
-    __device__ __forceinline__ int sweep_one(Isl& is, VC* vcs, int iters, bool early_exit) {
+    MRP_SOLVE_FN int sweep_one(Isl& is, VC* vcs, int iters, bool early_exit) {
         CC c = load_cc(vcs[0]);
         const int ia = vcs[0].iaI, ib = vcs[0].ibI;
         P2 vA = p2(is.vvx[ia], is.vvy[ia]); float wA = is.vw[ia];
@@ -1355,7 +1368,7 @@ template <int ENV> struct World {
     // other body of contact 0 and Z that of contact 1; X's role (A or B) in each contact is a
     // template parameter, so every body access is a register.
     template <bool XA0, bool XA1, int P0, int P1>
-    __device__ __forceinline__ int sweep_two(Isl& is, VC* vcs, int iters, bool early_exit, int x, int y, int z) {
+    MRP_SOLVE_FN int sweep_two(Isl& is, VC* vcs, int iters, bool early_exit, int x, int y, int z) {
         CC c0 = load_cc(vcs[0]), c1 = load_cc(vcs[1]);
         P2 vX = p2(is.vvx[x], is.vvy[x]), vY = p2(is.vvx[y], is.vvy[y]), vZ = p2(is.vvx[z], is.vvy[z]);
         float wX = is.vw[x], wY = is.vw[y], wZ = is.vw[z];
@@ -1384,7 +1397,7 @@ template <int ENV> struct World {
     // Two contacts between the same two bodies (e.g. an agent against both boxes of the T block):
     // contact 1 is (P, Q) when SAME, else (Q, P).
     template <bool SAME, int P0, int P1>
-    __device__ __forceinline__ int sweep_same(Isl& is, VC* vcs, int iters, bool early_exit, int p, int q) {
+    MRP_SOLVE_FN int sweep_same(Isl& is, VC* vcs, int iters, bool early_exit, int p, int q) {
         CC c0 = load_cc(vcs[0]), c1 = load_cc(vcs[1]);
         P2 vP = p2(is.vvx[p], is.vvy[p]), vQ = p2(is.vvx[q], is.vvy[q]);
         float wP = is.vw[p], wQ = is.vw[q];
@@ -1551,7 +1564,7 @@ template <int ENV> struct World {
     // XA1 else (Q, P)); otherwise X (= P) shared, Y (= Q) the other body of contact 0, Z of contact 1,
     // X's role in contact k given by XA0 / XA1.
     template <int NC, bool SAMEB, bool XA0, bool XA1>
-    __device__ __forceinline__ int pos_sweep(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB, int iters,
+    MRP_SOLVE_FN int pos_sweep(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB, int iters,
                                              int p, int q, int z) {
         PCC c0 = load_pcc(vcs[0], pcs[0], toi, toiA, toiB);
         PCC c1 = load_pcc(vcs[NC - 1], pcs[NC - 1], toi, toiA, toiB);
@@ -1603,7 +1616,7 @@ template <int ENV> struct World {
     // position passes of islands of NC = 3 or 4 contacts with the schedule (bodies, point counts,
     // manifold types) read out of the lanes once, before the passes (see lanes_sweeps)
     template <int NC>
-    __device__ __forceinline__ int lanes_passes(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB, int iters) {
+    MRP_LANES_FN int lanes_passes(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB, int iters) {
         const int me = tid < NC ? tid : 0;
         const PCC my = load_pcc(vcs[me], pcs[me], toi, toiA, toiB);
         const int cia = vcs[me].iaI, cib = vcs[me].ibI;
