@@ -28,8 +28,9 @@ DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("mrp_math.h", "mrp_config.h", 
 # lanes-path update's s_nop wait states from about 40 to 17, +5.7 % env-steps/s in the driver window
 # and +6.6 % at steps 21-220 (A/B, profiles/r3g_ab_scheduler.txt).  For v0 the same build gives
 # +1.5 % in the driver window but -2.7 % at steps 21-220 (a call per island solve), so v0 keeps the
-# inlined form.
-UNIT_FLAGS = {"mrp_env4.hip": ["-DMRP_SOLVE_NOINLINE_LANES", "-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
+# inlined form.  Heavy-v0 (env 1, 5 agents): +1.4 % / +2.0 % (profiles/r3g_ab_scheduler.txt).
+_ILP_LOOPS = ["-DMRP_SOLVE_NOINLINE_LANES", "-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+UNIT_FLAGS = {"mrp_env1.hip": _ILP_LOOPS, "mrp_env4.hip": _ILP_LOOPS}
 # -fno-slp-vectorize: the serial solver chains are latency-bound; packing pairs of f32 ops into
 # v_pk_* costs operand-shuffling moves on the dependency chain (measured +2-3 % env-steps/s off)
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",

@@ -38,6 +38,13 @@ constexpr int NULLN = -1;
 #else
 #define MRP_LANES_FN MRP_SOLVE_FN
 #endif
+// MRP_SOLVE_NOINLINE_MAIN (A/B): only the main island solve's lanes-path loops out of line (the TOI
+// sub-step solves keep them inlined)
+#ifdef MRP_SOLVE_NOINLINE_MAIN
+#define MRP_MAIN_FN __device__ __attribute__((noinline))
+#else
+#define MRP_MAIN_FN __device__ __forceinline__
+#endif
 
 // v_writelane_b32 (clang exposes no builtin for it; the LLVM intrinsic is bound by name, so the
 // compiler still inserts the readlane -> writelane wait states itself)
@@ -1100,11 +1107,15 @@ template <int ENV> struct World {
         if (tid < NC) store_cc(vcs[tid], my);
         return sweeps;
     }
+    template <int NC>
+    MRP_MAIN_FN int lanes_sweeps_main(Isl& is, VC* vcs, int iters, bool early_exit) { return lanes_sweeps<NC>(is, vcs, iters, early_exit); }
+    // MAIN: the call of the main island solve (b2Island::Solve), not a TOI sub-step's
+    template <bool MAIN = false>
     __device__ __forceinline__ int solver_velocity_lanes(Isl& is, VC* vcs, int iters, bool early_exit = true) {
         {
             const int n = __builtin_amdgcn_readfirstlane(is.nc);
-            if (n == 3) return lanes_sweeps<3>(is, vcs, iters, early_exit);
-            if (n == 4) return lanes_sweeps<4>(is, vcs, iters, early_exit);
+            if (n == 3) return MAIN ? lanes_sweeps_main<3>(is, vcs, iters, early_exit) : lanes_sweeps<3>(is, vcs, iters, early_exit);
+            if (n == 4) return MAIN ? lanes_sweeps_main<4>(is, vcs, iters, early_exit) : lanes_sweeps<4>(is, vcs, iters, early_exit);
             if constexpr (SCHED_WIDE) {   // islands of 5-8 contacts (the 3-block config: +4 %)
                 if (n == 5) return lanes_sweeps<5>(is, vcs, iters, early_exit);
                 if (n == 6) return lanes_sweeps<6>(is, vcs, iters, early_exit);
@@ -1647,13 +1658,18 @@ template <int ENV> struct World {
         if (tid < is.nb) { is.pcx[tid] = bx; is.pcy[tid] = by; is.pa[tid] = ba; }
         return it;
     }
+    template <int NC>
+    MRP_MAIN_FN int lanes_passes_main(Isl& is, const VC* vcs, const PC* pcs, int iters) {
+        return lanes_passes<NC>(is, vcs, pcs, false, -1, -1, iters);
+    }
+    template <bool MAIN = false>
     __device__ __forceinline__ int solver_position_lanes(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB, int iters) {
         // single-block envs only: in the 3-block config the scheduled passes measured slower (-2.7 %,
         // also with 5-8 contact islands scheduled; profiles/r3g_ab_env4_schedules.txt)
         if constexpr (NB == 1) {
             const int n = __builtin_amdgcn_readfirstlane(is.nc);
-            if (n == 3) return lanes_passes<3>(is, vcs, pcs, toi, toiA, toiB, iters);
-            if (n == 4) return lanes_passes<4>(is, vcs, pcs, toi, toiA, toiB, iters);
+            if (n == 3) return MAIN ? lanes_passes_main<3>(is, vcs, pcs, iters) : lanes_passes<3>(is, vcs, pcs, toi, toiA, toiB, iters);
+            if (n == 4) return MAIN ? lanes_passes_main<4>(is, vcs, pcs, iters) : lanes_passes<4>(is, vcs, pcs, toi, toiA, toiB, iters);
         }
         const int nc = is.nc;
         const int me = tid < nc ? tid : 0;   // lanes >= nc evaluate a copy of contact 0 and are never kept
@@ -1748,7 +1764,7 @@ template <int ENV> struct World {
     __device__ __forceinline__ void island_position(Isl& is, VC* vcs, PC* pcs, int nc) {
         if (nc > 0 && nc <= 64) {
             int n = solver_position_small(is, vcs, pcs, false, -1, -1, 60);
-            if (n < 0) n = solver_position_lanes(is, vcs, pcs, false, -1, -1, 60);
+            if (n < 0) n = solver_position_lanes<true>(is, vcs, pcs, false, -1, -1, 60);
             if (tid == 0) S.posIters += n;
         } else if (tid == 0) {
             if (nc > 0) {
@@ -1835,7 +1851,7 @@ template <int ENV> struct World {
             if (nc > 0 && nc <= 64) {
                 set_prio(lvl > step_prio ? lvl : step_prio);
                 int sweeps = nc == 1 ? solver_velocity_one(is, sh.u.sol.vcs, 180) : (nc == 2 ? solver_velocity_two(is, sh.u.sol.vcs, 180) : -1);
-                if (sweeps < 0) sweeps = solver_velocity_lanes(is, sh.u.sol.vcs, 180);
+                if (sweeps < 0) sweeps = solver_velocity_lanes<true>(is, sh.u.sol.vcs, 180);
                 MRP_TRACE(15, sweeps * nc);
                 (void)sweeps;
             }
