@@ -33,6 +33,10 @@ ENV_NAMES = {0: "MultiRobotPuzzle-v0", 1: "MultiRobotPuzzleHeavy-v0", 2: "MultiR
 # once per step plus I/O; shared geometry/mass tables excluded.
 ALGO_BYTES = {0: 1657, 1: 3547, 2: 3613, 3: 3613, 4: 6085, 5: 1653, 6: 1653}   # v3: v0's lane state, 27-float obs
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
+# the gym-style single env of each config (make() id and constructor arguments) for the drop-in diagnostic
+SINGLE_ENV_MAKE = {0: ("MultiRobotPuzzle-v0", {}), 1: ("MultiRobotPuzzleHeavy-v0", {}), 2: ("MultiRobotPuzzle-v2", {}),
+                   3: ("MultiRobotPuzzleHeavy-v2", {}), 4: ("MultiRobotPuzzleHeavy-v2-3block", {}),
+                   5: ("MultiRobotPuzzle-v3", {}), 6: ("MultiRobotPuzzle-v3", {"heavy": True})}
 
 
 def host_cpus() -> dict:
@@ -66,37 +70,78 @@ def host_cpus() -> dict:
             "allotted": allot, "rule": rule}
 
 
-def cpu_baseline(env_id: int, lanes: int, seed: int, target_s: float = 15.0, single_s: float = 4.0) -> dict:
-    """Time the CPU oracle (plain-C restatement, OpenMP over lanes) on a bounded sample of the
-    same workload: same env, same lane count, same counter-RNG actions/spawns and auto-reset as
-    the GPU run, on all allotted host cores, for as many steps as fit in about `target_s` seconds;
-    then one lane on one core (BASELINE.json configs[0]) for about `single_s` seconds."""
+def _oracle_rate(variant: str, env_id: int, lanes: int, skip: int, steps: int, seed: int, threads: int, target_s: float,
+                 max_reps: int) -> dict:
+    """Time one oracle build (oracle/Makefile variant) on `lanes` lanes x steps skip+1 .. skip+steps
+    after spawn, the same counter-RNG workload as the GPU line; repetition r uses seed + r (r = 0 is
+    exactly the GPU's lanes), repeated until about `target_s` seconds of timed work."""
     from gym_puzzles_amd.spawn import draw_bounds
     from oracle.oracle import batch_run  # test infrastructure: baseline leg only
+    bounds = draw_bounds(env_id)
+    # one untimed repetition first: the first pass over fresh worlds pays page faults and allocator
+    # growth (4-5x slower on the first call in a process), which is not the step's cost
+    batch_run(env_id, lanes, steps, seed, bounds, threads=threads, skip=skip, variant=variant)
+    n_tot, dt_tot, reps, rep0 = 0, 0.0, 0, None
+    while reps < max_reps and (reps == 0 or dt_tot < target_s):
+        n, dt = batch_run(env_id, lanes, steps, seed + reps, bounds, threads=threads, skip=skip, variant=variant)
+        n_tot, dt_tot, reps = n_tot + n, dt_tot + dt, reps + 1
+        if rep0 is None:
+            rep0 = n / max(dt, 1e-9)
+    return {"value": n_tot / max(dt_tot, 1e-9), "seconds": dt_tot, "env_steps": n_tot, "reps": reps,
+            "seeds": [seed, seed + reps - 1], "first_rep_value": rep0}
+
+
+def cpu_baseline(env_id: int, lanes: int, seed: int, skip: int, steps: int, episode: bool = True,
+                 target_s: float = 8.0) -> dict:
+    """The CPU baseline (cpu_baseline in the JSON line), timed like for like with the GPU line:
+    the C restatement of the step (oracle/, kind "port": pybox2d cannot run here or on the GPU
+    box) built WITHOUT the work model (oracle/Makefile libmrp_oracle_port.so: the Box2D algorithm,
+    all 180 velocity sweeps as b2Island::Solve runs them), on all allotted host cores, over the
+    GPU line's own window -- the same lanes, steps skip+1 .. skip+steps after spawn, the same
+    counter-RNG spawns and actions, auto-reset -- repeated over seeds to ~target_s seconds.
+    Beside it (never `value`): the same build over one whole episode; the early-exit port
+    (libmrp_oracle_early.so: the device's exact period-1/2 exit of the velocity sweeps, same bits)
+    on the same window and episode, so GPU / CPU separates the hardware from that algorithmic
+    saving; and one lane on one core (BASELINE.json configs[0])."""
+    from gym_puzzles_amd.spawn import draw_bounds
+    from oracle.oracle import batch_run, build_kind, lib  # test infrastructure: baseline leg only
     cpus = host_cpus()
     threads = cpus["allotted"]
+    port = _oracle_rate("port", env_id, lanes, skip, steps, seed, threads, target_s, 400)
+    early = _oracle_rate("early", env_id, lanes, skip, steps, seed, threads, target_s / 2, 400)
+    out = {"value": port["value"], "unit": "env-steps/s", "cores": threads, "kind": "port",
+           "sample": f"{ENV_NAMES[env_id]}: {lanes} lanes x steps {skip + 1}-{skip + steps} after spawn (the GPU line's "
+                     f"window; device-RNG actions and spawns, auto-reset), {port['reps']} repetitions over seeds "
+                     f"{port['seeds'][0]}-{port['seeds'][1]} (seed {seed} = the GPU's lanes), {threads} OpenMP threads, "
+                     f"{port['seconds']:.1f} s timed; build oracle/build/libmrp_oracle_port.so ({build_kind('port')})",
+           "window": port, "host_cpus": cpus,
+           "early_exit_port": dict(early, build=build_kind("early"),
+                                   note="same window and bits; velocity sweeps stop at the device's exact early exit")}
     bounds = draw_bounds(env_id)
-    n, dt = batch_run(env_id, min(lanes, 32 * threads), 20, seed, bounds, threads=threads)    # calibrate
-    rate = n / max(dt, 1e-6)
-    steps = int(max(20, min(20000, target_s * rate / lanes)))
-    n, dt = batch_run(env_id, lanes, steps, seed, bounds, threads=threads)
-    n1, dt1 = batch_run(env_id, 1, 200, seed, bounds, threads=1)
-    steps1 = int(max(200, min(200000, single_s * n1 / max(dt1, 1e-6))))
-    n1, dt1 = batch_run(env_id, 1, steps1, seed, bounds, threads=1)
-    return {"value": n / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{ENV_NAMES[env_id]}: {lanes} lanes x {steps} steps (device-RNG actions and spawns, "
-                      f"auto-reset) of the C oracle (oracle/), {threads} OpenMP threads, {dt:.1f} s",
-            "host_cpus": cpus,
-            "single_lane_1core": {"value": n1 / dt1, "unit": "env-steps/s", "cores": 1,
-                                  "sample": f"1 lane x {steps1} steps of the same workload, 1 thread, {dt1:.1f} s "
-                                            "(BASELINE.json configs[0]: 1 env on the CPU)"}}
+    T = lib("port").or_max_episode_steps(env_id)
+    if episode:
+        eps = {}
+        for v in ("port", "early"):
+            n, dt = batch_run(env_id, lanes, T, seed, bounds, threads=threads, variant=v)
+            eps[v] = {"steps": T, "value": n / max(dt, 1e-9), "seconds": dt}
+        out["whole_episode"] = eps
+    # one lane on one core: whole episodes over seeds, about 3 s
+    n1, dt1, r1 = 0, 0.0, 0
+    while dt1 < 3.0 and r1 < 200:
+        n, dt = batch_run(env_id, 1, T, seed + r1, bounds, threads=1, variant="port")
+        n1, dt1, r1 = n1 + n, dt1 + dt, r1 + 1
+    out["single_lane_1core"] = {"value": n1 / max(dt1, 1e-9), "unit": "env-steps/s", "cores": 1,
+                                "sample": f"1 lane x {T} steps (one whole episode) x {r1} seeds of the same workload, "
+                                          f"port build, 1 thread, {dt1:.1f} s (BASELINE.json configs[0]: 1 env on the CPU)"}
+    return out
 
 
-def single_env_rate(env_name: str, steps: int = 300) -> dict:
+def single_env_rate(env_id: int, steps: int = 300) -> dict:
     """Diagnostic (never `value`): the gym-style drop-in path, `make(id)` then env.step(a) with host
     numpy actions - one lane per call, PCIe round trip included (what train.py's DummyVecEnv drives)."""
     from gym_puzzles_amd import make
-    env = make(env_name)
+    name, kw = SINGLE_ENV_MAKE[env_id]
+    env = make(name, **kw)
     env.reset()
     rs = np.random.RandomState(0)
     acts = rs.uniform(-1, 1, size=(steps + 20, env.action_space.shape[0])).astype(np.float32)
@@ -112,7 +157,8 @@ def single_env_rate(env_name: str, steps: int = 300) -> dict:
     dt = time.perf_counter() - t0
     env.close()
     return {"env_steps_per_s": steps / dt, "us_per_step": dt / steps * 1e6, "steps": steps,
-            "path": f"gym_puzzles_amd.make('{env_name}').step(): 1-lane kernel + host copies per call"}
+            "path": f"gym_puzzles_amd.make('{name}'{''.join(f', {k}={v!r}' for k, v in kw.items())}).step(): "
+                    "1-lane kernel, actions and outputs through the ctx's pinned host buffer"}
 
 
 def load_valu_latency(env_id: int, lanes: int, first: int, last: int, seed: int, kern_ms: float):
@@ -240,6 +286,7 @@ def main():
     for _ in range(args.warmup):
         one_step()
     torch.cuda.synchronize(dev)
+    ctr0 = b.counters_ex()   # the batch counters count from creation: the timed window is the difference
 
     K = args.steps
     # kernel_ms: k_step's mean launch duration over exactly the K timed launches.  When k_step is
@@ -288,9 +335,11 @@ def main():
     # the run must not hide a broken lane: loop-guard faults and non-finite outputs are checked
     # over the timed window (status bit MRP_STATUS_NONFINITE marks a lane-step with NaN/inf)
     flt = b.faults()
+    ctr1 = b.counters_ex()
+    ctr_window = {k: ctr1[k] - ctr0[k] for k in ctr1}
     bad = {"lanes_with_loop_guard_fault": int(np.count_nonzero(flt)),
            "obs_finite": bool(torch.isfinite(obs).all().item()),
-           "nonfinite_lane_steps": int(b.counters_ex()["nonfinite_steps"])}
+           "nonfinite_lane_steps": int(ctr_window["nonfinite_steps"])}
     if distributed:
         t = torch.tensor([elapsed, kern_ms, bad["lanes_with_loop_guard_fault"], 0 if bad["obs_finite"] else 1,
                           bad["nonfinite_lane_steps"]], dtype=torch.float64, device=dev)
@@ -299,7 +348,7 @@ def main():
         bad = {"lanes_with_loop_guard_fault": int(t[2]), "obs_finite": not bool(t[3]), "nonfinite_lane_steps": int(t[4])}
     checks_ok = bad["lanes_with_loop_guard_fault"] == 0 and bad["obs_finite"] and bad["nonfinite_lane_steps"] == 0
 
-    ctr = b.counters_ex() if rank == 0 else {}
+    ctr = {"timed_window": ctr_window, "since_creation": ctr1} if rank == 0 else {}
     # Diagnostics only (never `value`): the rate over a later window of the same episodes (every
     # lane spawned at step 0; the first tens of steps after a spawn carry most of the overlap
     # resolution, so a window's rate depends on where it sits).
@@ -369,7 +418,7 @@ def main():
                  "ratio": rates["multi"] / rates["single"]}
     single = None
     if args.single_env > 0 and rank == 0 and not distributed:
-        single = single_env_rate(ENV_NAMES[args.env] if args.env < 4 else "MultiRobotPuzzle-v0", args.single_env)
+        single = single_env_rate(args.env, args.single_env)
     if rank == 0:
         total_steps = world * L * K
         value = total_steps / elapsed
@@ -413,7 +462,9 @@ def main():
                             "single_env_drop_in": single},
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.env, L, args.seed)
+            line["cpu_baseline"] = cpu_baseline(args.env, L, args.seed, args.warmup, K)
+            cb = line["cpu_baseline"]
+            cb["gpu_over_cpu"] = {"port": value / cb["value"], "early_exit_port": value / cb["early_exit_port"]["value"]}
         print(json.dumps(line), flush=True)
     b.close()
     if distributed:

@@ -95,8 +95,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.mrp_set_seed.argtypes = [P, u64]
     L.mrp_set_schedule.argtypes = [P, i]
     L.mrp_set_auto_reset.argtypes = [P, i]
-    if hasattr(L, "mrp_set_frameskip"):   # absent from libraries built before round 3 (A/B baselines)
-        L.mrp_set_frameskip.argtypes = [P, i]
+    L.mrp_set_frameskip.argtypes = [P, i]
     L.mrp_get_bodies.argtypes = [P, P]
     L.mrp_get_flags.argtypes = [P, P]
     L.mrp_get_faults.argtypes = [P, P]
@@ -125,10 +124,12 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.mrp_norm_step_device_ex.argtypes = [P] * 11
     L.mrp_norm_get_stats.argtypes = [P, P]
     L.mrp_norm_set_stats.argtypes = [P, P]
-    for name, args in (("mrp_debug_stamps_ext", [i, P, P, P]), ("mrp_debug_trace", [i, P, i]),
-                       ("mrp_debug_progress", [i, ctypes.POINTER(P), i]), ("mrp_debug_velbench", [i, i, i, i, i, P])):
-        if hasattr(L, name):   # diagnostics: absent from older builds
-            getattr(L, name).argtypes = args
+    # every build exports the whole ABI of include/mrp.h (the diagnostics answer MRP_E_STATE outside
+    # their -D builds), so an A/B library must be built from this ABI too: a missing symbol raises here
+    L.mrp_debug_stamps_ext.argtypes = [i, P, P, P]
+    L.mrp_debug_trace.argtypes = [i, P, i]
+    L.mrp_debug_progress.argtypes = [i, ctypes.POINTER(P), i]
+    L.mrp_debug_velbench.argtypes = [i, i, i, i, i, P]
     _lib = L
     return L
 
@@ -177,6 +178,12 @@ class Batch:
         self.truncated = np.zeros(n_lanes, np.uint8)
         self.status = np.zeros(n_lanes, np.uint8)
         self.terminal_obs = np.zeros((n_lanes, self.obs_dim), np.float32)
+        # the output arrays live as long as the batch: their addresses are taken once, so a host step
+        # costs one ctypes call (the gym-style single env steps one lane per call)
+        self._L = L
+        self._out = (self.obs.ctypes.data, self.reward.ctypes.data, self.reward64.ctypes.data, self.done.ctypes.data,
+                     self.truncated.ctypes.data, self.status.ctypes.data)
+        self._term = self.terminal_obs.ctypes.data
 
     def _check(self, rc):
         if rc != MRP_OK:
@@ -230,10 +237,16 @@ class Batch:
         return self.obs
 
     def step(self, actions=None, want_terminal_obs=False):
-        a = None if actions is None else np.ascontiguousarray(actions, np.float32).reshape(self.n_lanes, self.act_dim)
-        term = self.terminal_obs if want_terminal_obs else None
-        self._check(load().mrp_step_ex(self._h, _p(a), _p(self.obs), _p(self.reward), _p(self.reward64), _p(self.done),
-                                       _p(self.truncated), _p(self.status), _p(term)))
+        if actions is None:
+            ap = None
+        else:
+            a = np.ascontiguousarray(actions, np.float32)
+            if a.size != self.n_lanes * self.act_dim:
+                raise ValueError(f"actions: expected {self.n_lanes} x {self.act_dim} values, got shape {a.shape}")
+            ap = a.ctypes.data
+        rc = self._L.mrp_step_ex(self._h, ap, *self._out, self._term if want_terminal_obs else None)
+        if rc != MRP_OK:
+            self._check(rc)
         return self.obs, self.reward, self.done, self.truncated
 
     def step_device(self, d_actions, d_obs, d_reward=None, d_done=None, d_trunc=None, d_status=None, d_term=None,

@@ -71,21 +71,43 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
         keep = {f"mrp_env{e}.hip" for e in only_envs}
         base = os.path.join(HERE, "build", os.path.basename(OUT) + ".obj")
         todo = [i for i, s in enumerate(SOURCES) if "mrp_env" not in s or os.path.basename(s) in keep]
+        # the reused objects must have been compiled from the current sources and headers: an env
+        # unit built before a shared header changed would mix two layouts in one A/B library
+        newest_dep = max(os.path.getmtime(d) for d in DEPS if os.path.exists(d) and d.endswith((".h", ".hip", ".cpp")))
         for i, s in enumerate(SOURCES):
             if i not in todo:
                 objs[i] = os.path.join(base, os.path.basename(s) + ".o")
                 if not os.path.exists(objs[i]):
                     raise FileNotFoundError(f"{objs[i]}: build the default library first")
+                if os.path.getmtime(objs[i]) < newest_dep:
+                    raise RuntimeError(f"{objs[i]} is older than a source or header it depends on: rebuild the default "
+                                       "library (python -m gym_puzzles_amd.build) before a variant")
 
     # A/B only: extra compiler flags for a variant library (never the default one)
     extra = os.environ.get("MRP_EXTRA_FLAGS", "").split() if out != OUT else []
 
+    headers = [d for d in DEPS if d.endswith(".h")]
+    newest_header = max(os.path.getmtime(d) for d in headers if os.path.exists(d))
+
     def compile_one(i: int) -> None:
         unit = UNIT_FLAGS.get(os.path.basename(SOURCES[i]), []) if not extra else []
         cmd = [hipcc()] + FLAGS + unit + extra + dflags + ["-c", SOURCES[i], "-o", objs[i]]
+        # incremental: an object newer than its source and every header, built with the same command
+        # line (recorded beside it), is kept; the env units include every header, so a header edit
+        # rebuilds them all, while an edit of mrp_kernels.hip alone rebuilds that unit only
+        stamp = objs[i] + ".cmd"
+        line = " ".join(cmd)
+        if not force and os.path.exists(objs[i]) and os.path.exists(stamp):
+            t = os.path.getmtime(objs[i])
+            with open(stamp) as f:
+                same = f.read() == line
+            if same and t >= os.path.getmtime(SOURCES[i]) and t >= newest_header:
+                return
         if verbose:
-            print(" ".join(cmd), flush=True)
+            print(line, flush=True)
         subprocess.run(cmd, check=True)
+        with open(stamp, "w") as f:
+            f.write(line)
 
     # slowest units first; each hipcc is single-threaded, so one job per core
     jobs = jobs or max(1, min(len(SOURCES), os.cpu_count() or 1, int(os.environ.get("MAX_JOBS", "16"))))
@@ -101,15 +123,15 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
 
 
 if __name__ == "__main__":
-    if "--stamps" in sys.argv:   # diagnostic per-phase timing build (tools/phase_profile.py)
-        print(build(force=True, verbose=True, out=os.path.join(HERE, "libmrp_stamps.so"), defines=("MRP_STAMPS",)))
+    if "--stamps" in sys.argv:   # diagnostic per-phase timing build (tools/phase_profile.py; --variant builds fewer units)
+        print(build(verbose=True, out=os.path.join(HERE, "libmrp_stamps.so"), defines=("MRP_STAMPS",)))
     elif "--progress" in sys.argv:   # diagnostic hang-localisation build (tools/hang_probe.py)
-        print(build(force=True, verbose=True, out=os.path.join(HERE, "libmrp_progress.so"), defines=("MRP_PROGRESS",)))
+        print(build(verbose=True, out=os.path.join(HERE, "libmrp_progress.so"), defines=("MRP_PROGRESS",)))
     elif "--variant" in sys.argv:   # A/B library: python -m gym_puzzles_amd.build --variant OUT.so E [E ...] [-DNAME ...]
         i = sys.argv.index("--variant")
         args = sys.argv[i + 2:]
         envs = [int(a) for a in args if not a.startswith("-D")]
         defs = [a[2:] for a in args if a.startswith("-D")]
-        print(build(force=True, verbose=True, out=os.path.abspath(sys.argv[i + 1]), defines=defs, only_envs=envs))
+        print(build(verbose=True, out=os.path.abspath(sys.argv[i + 1]), defines=defs, only_envs=envs))
     else:
-        print(build(force="--force" in sys.argv, verbose=True))
+        print(build(force="--force" in sys.argv, verbose=True))   # --force: recompile every unit

@@ -91,17 +91,24 @@ struct mrp_ctx {
     double base_puzzle = 10000.0, base_bounds = 1000.0, base_blk_bounds = 100.0;   // set_reward_params
     int shaped_set = 0;                                                             // update_params() called
     int obs_dim = 0, act_dim = 0, n_draws = 0, n_agents = 0, n_blocks = 0, max_steps = 0, words = 0;
-    // staging buffers for the host-pointer API
-    double* d_draws = nullptr;
-    float* d_actions = nullptr;
-    uint8_t* d_mask = nullptr;
-    float* d_obs = nullptr;
-    float* d_reward = nullptr;
-    double* d_reward64 = nullptr;
-    uint8_t* d_done = nullptr;
-    uint8_t* d_trunc = nullptr;
-    uint8_t* d_status = nullptr;
-    float* d_term = nullptr;
+    // The host-pointer API's I/O: one pinned, device-mapped host buffer (hipHostMalloc) that the
+    // kernels read their inputs from and write their outputs to directly over PCIe, so a host step is
+    // one launch and one synchronisation -- no staging copies (the gym-style single env path,
+    // train.py:63-80's DummyVecEnv, steps one lane per call).  h_* are host addresses, dev() maps
+    // them to the device address of the same bytes.
+    uint8_t* h_io = nullptr;
+    uint8_t* d_io = nullptr;
+    double* h_draws = nullptr;
+    float* h_actions = nullptr;
+    uint8_t* h_mask = nullptr;
+    float* h_obs = nullptr;
+    float* h_term = nullptr;
+    float* h_reward = nullptr;
+    double* h_reward64 = nullptr;
+    uint8_t* h_done = nullptr;
+    uint8_t* h_trunc = nullptr;
+    uint8_t* h_status = nullptr;
+    template <class T> T* dev(T* h) const { return h ? reinterpret_cast<T*>(d_io + (reinterpret_cast<uint8_t*>(h) - h_io)) : nullptr; }
     float* d_bodies = nullptr;
     int32_t* d_flags = nullptr;
     int64_t* d_ctr = nullptr;    // [CTR_N] mrp_counters_ex
@@ -154,10 +161,10 @@ void mrp_destroy(mrp_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    void* bufs[] = {ctx->d_state, ctx->d_draws, ctx->d_actions, ctx->d_mask, ctx->d_obs, ctx->d_reward, ctx->d_reward64,
-                    ctx->d_done, ctx->d_trunc, ctx->d_status, ctx->d_term, ctx->d_bodies, ctx->d_flags, ctx->d_ctr};
+    void* bufs[] = {ctx->d_state, ctx->d_bodies, ctx->d_flags, ctx->d_ctr};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
+    if (ctx->h_io) (void)hipHostFree(ctx->h_io);
     if (ctx->d_order) (void)hipFree(ctx->d_order);
     if (ctx->d_cost) (void)hipFree(ctx->d_cost);
     if (ctx->d_costmax) (void)hipFree(ctx->d_costmax);
@@ -210,22 +217,34 @@ int mrp_create(int env_id, int n_lanes, int device, uint64_t seed, uint64_t lane
     size_t nl = (size_t)n_lanes;
     struct { void** p; size_t bytes; } allocs[] = {
         {(void**)&ctx->d_state, (size_t)ctx->words * nl * 4},
-        {(void**)&ctx->d_draws, nl * ctx->n_draws * sizeof(double)},
-        {(void**)&ctx->d_actions, nl * ctx->act_dim * sizeof(float)},
-        {(void**)&ctx->d_mask, nl},
-        {(void**)&ctx->d_obs, nl * ctx->obs_dim * sizeof(float)},
-        {(void**)&ctx->d_term, nl * ctx->obs_dim * sizeof(float)},
-        {(void**)&ctx->d_reward, nl * sizeof(float)},
-        {(void**)&ctx->d_reward64, nl * sizeof(double)},
-        {(void**)&ctx->d_done, nl},
-        {(void**)&ctx->d_trunc, nl},
-        {(void**)&ctx->d_status, nl},
         {(void**)&ctx->d_bodies, nl * 6 * (ctx->n_agents + ctx->n_blocks) * sizeof(float)},
         {(void**)&ctx->d_flags, nl * (ctx->n_agents + 1) * sizeof(int32_t)},
         {(void**)&ctx->d_ctr, CTR_N * sizeof(int64_t)},
     };
     for (auto& a : allocs)
         if ((e = hipMalloc(a.p, a.bytes)) != hipSuccess) return fail("hipMalloc", e);
+    {   // the host API's pinned I/O buffer, carved 16-B aligned: doubles first, then floats, then bytes
+        auto up = [](size_t b) { return (b + 15) & ~(size_t)15; };
+        const size_t sz_draws = up(nl * ctx->n_draws * sizeof(double)), sz_r64 = up(nl * sizeof(double));
+        const size_t sz_act = up(nl * ctx->act_dim * sizeof(float)), sz_obs = up(nl * ctx->obs_dim * sizeof(float));
+        const size_t sz_rew = up(nl * sizeof(float)), sz_b = up(nl);
+        const size_t bytes = sz_draws + sz_r64 + sz_act + 2 * sz_obs + sz_rew + 4 * sz_b;
+        if ((e = hipHostMalloc((void**)&ctx->h_io, bytes, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+            return fail("hipHostMalloc", e);
+        if ((e = hipHostGetDevicePointer((void**)&ctx->d_io, ctx->h_io, 0)) != hipSuccess) return fail("hipHostGetDevicePointer", e);
+        std::memset(ctx->h_io, 0, bytes);
+        uint8_t* q = ctx->h_io;
+        ctx->h_draws = (double*)q; q += sz_draws;
+        ctx->h_reward64 = (double*)q; q += sz_r64;
+        ctx->h_actions = (float*)q; q += sz_act;
+        ctx->h_obs = (float*)q; q += sz_obs;
+        ctx->h_term = (float*)q; q += sz_obs;
+        ctx->h_reward = (float*)q; q += sz_rew;
+        ctx->h_mask = q; q += sz_b;
+        ctx->h_done = q; q += sz_b;
+        ctx->h_trunc = q; q += sz_b;
+        ctx->h_status = q;
+    }
     if ((e = hipMalloc((void**)&ctx->d_order, nl * sizeof(int))) != hipSuccess) return fail("hipMalloc", e);
     if ((e = hipMalloc((void**)&ctx->d_cost, nl * sizeof(uint32_t))) != hipSuccess) return fail("hipMalloc", e);
     if ((e = hipMalloc((void**)&ctx->d_costmax, sizeof(uint32_t))) != hipSuccess) return fail("hipMalloc", e);
@@ -317,18 +336,17 @@ int mrp_reset(mrp_ctx* ctx, const uint8_t* mask, const double* draws, const floa
     if (!ctx || !obs) return MRP_E_ARG;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     size_t nl = (size_t)ctx->n_lanes;
-    if (mask) HIPCHK(ctx, hipMemcpyAsync(ctx->d_mask, mask, nl, hipMemcpyHostToDevice, ctx->stream));
-    if (draws)
-        HIPCHK(ctx, hipMemcpyAsync(ctx->d_draws, draws, nl * ctx->n_draws * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-    if (actions)
-        HIPCHK(ctx, hipMemcpyAsync(ctx->d_actions, actions, nl * ctx->act_dim * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    // inputs into the pinned I/O buffer; the kernel reads them and writes the reset rows there
+    if (mask) std::memcpy(ctx->h_mask, mask, nl);
+    if (draws) std::memcpy(ctx->h_draws, draws, nl * ctx->n_draws * sizeof(double));
+    if (actions) std::memcpy(ctx->h_actions, actions, nl * ctx->act_dim * sizeof(float));
     // rows of unmasked lanes stay as the caller had them
-    HIPCHK(ctx, hipMemcpyAsync(ctx->d_obs, obs, nl * ctx->obs_dim * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
-    int rc = mrp_reset_device(ctx, mask ? ctx->d_mask : nullptr, draws ? ctx->d_draws : nullptr,
-                              actions ? ctx->d_actions : nullptr, ctx->d_obs);
+    if (mask) std::memcpy(ctx->h_obs, obs, nl * ctx->obs_dim * sizeof(float));
+    int rc = mrp_reset_device(ctx, mask ? ctx->dev(ctx->h_mask) : nullptr, draws ? ctx->dev(ctx->h_draws) : nullptr,
+                              actions ? ctx->dev(ctx->h_actions) : nullptr, ctx->dev(ctx->h_obs));
     if (rc) return rc;
-    HIPCHK(ctx, hipMemcpyAsync(obs, ctx->d_obs, nl * ctx->obs_dim * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    std::memcpy(obs, ctx->h_obs, nl * ctx->obs_dim * sizeof(float));
     return MRP_OK;
 }
 
@@ -376,21 +394,22 @@ int mrp_step_ex(mrp_ctx* ctx, const float* actions, float* obs, float* reward, d
     if (!ctx || !obs) return MRP_E_ARG;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     size_t nl = (size_t)ctx->n_lanes;
-    if (actions)
-        HIPCHK(ctx, hipMemcpyAsync(ctx->d_actions, actions, nl * ctx->act_dim * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
-    int rc = mrp_step_device_ex(ctx, actions ? ctx->d_actions : nullptr, ctx->d_obs, ctx->d_reward,
-                                reward64 ? ctx->d_reward64 : nullptr, ctx->d_done, ctx->d_trunc, ctx->d_status,
-                                term ? ctx->d_term : nullptr);
+    // one launch that reads the actions from and writes every output into the pinned I/O buffer,
+    // one synchronisation, then host copies out of it
+    if (actions) std::memcpy(ctx->h_actions, actions, nl * ctx->act_dim * sizeof(float));
+    int rc = mrp_step_device_ex(ctx, actions ? ctx->dev(ctx->h_actions) : nullptr, ctx->dev(ctx->h_obs),
+                                reward ? ctx->dev(ctx->h_reward) : nullptr, reward64 ? ctx->dev(ctx->h_reward64) : nullptr,
+                                done ? ctx->dev(ctx->h_done) : nullptr, trunc ? ctx->dev(ctx->h_trunc) : nullptr,
+                                status ? ctx->dev(ctx->h_status) : nullptr, term ? ctx->dev(ctx->h_term) : nullptr);
     if (rc) return rc;
-    HIPCHK(ctx, hipMemcpyAsync(obs, ctx->d_obs, nl * ctx->obs_dim * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
-    if (reward) HIPCHK(ctx, hipMemcpyAsync(reward, ctx->d_reward, nl * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
-    if (reward64) HIPCHK(ctx, hipMemcpyAsync(reward64, ctx->d_reward64, nl * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-    if (done) HIPCHK(ctx, hipMemcpyAsync(done, ctx->d_done, nl, hipMemcpyDeviceToHost, ctx->stream));
-    if (trunc) HIPCHK(ctx, hipMemcpyAsync(trunc, ctx->d_trunc, nl, hipMemcpyDeviceToHost, ctx->stream));
-    if (status) HIPCHK(ctx, hipMemcpyAsync(status, ctx->d_status, nl, hipMemcpyDeviceToHost, ctx->stream));
-    if (term)
-        HIPCHK(ctx, hipMemcpyAsync(term, ctx->d_term, nl * ctx->obs_dim * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    std::memcpy(obs, ctx->h_obs, nl * ctx->obs_dim * sizeof(float));
+    if (reward) std::memcpy(reward, ctx->h_reward, nl * sizeof(float));
+    if (reward64) std::memcpy(reward64, ctx->h_reward64, nl * sizeof(double));
+    if (done) std::memcpy(done, ctx->h_done, nl);
+    if (trunc) std::memcpy(trunc, ctx->h_trunc, nl);
+    if (status) std::memcpy(status, ctx->h_status, nl);
+    if (term) std::memcpy(term, ctx->h_term, nl * ctx->obs_dim * sizeof(float));
     return MRP_OK;
 }
 
@@ -458,7 +477,28 @@ int mrp_set_state(mrp_ctx* ctx, const uint32_t* in) {
     if (!ctx || !in) return MRP_E_ARG;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     size_t nl = (size_t)ctx->n_lanes, nw = (size_t)ctx->words;
-    HIPCHK(ctx, hipMemcpyAsync(ctx->d_state, in, nl * nw * 4, hipMemcpyHostToDevice, ctx->stream));
+    // k_step moves only the contact slots below a lane's high-water mark cHW and rebuilds the rest
+    // in LDS with their initial contents (mrp_lane.h StateIO), so a state whose cHW understates its
+    // highest non-initial slot would lose contacts silently.  Recompute the mark from the slots:
+    // 1 + the highest slot whose words differ from the initial ones (cnext[c] = c + 1 or NULL, every
+    // other array 0), never lower than the stored value (a higher mark only moves more words).
+    const EnvOps* o = env_ops(ctx->env_id);
+    std::vector<uint32_t> st(in, in + nl * nw);
+    const size_t C = (size_t)o->cslot_n;
+    for (size_t l = 0; l < nl; ++l) {
+        uint32_t* w = st.data() + l * nw;
+        int hw = 0;
+        for (size_t a = 0; a < (size_t)o->cslot_arrays; ++a)
+            for (size_t c = (size_t)hw; c < C; ++c) {
+                const uint32_t init = a == 0 ? (c + 1 < C ? (uint32_t)(c + 1) : 0xffffffffu) : 0u;
+                if (w[o->cslot_word + a * C + c] != init) hw = (int)c + 1;
+            }
+        int32_t mark;
+        std::memcpy(&mark, &w[o->chw_word], 4);
+        mark = std::max(std::min(mark, (int32_t)C), (int32_t)hw);
+        std::memcpy(&w[o->chw_word], &mark, 4);
+    }
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_state, st.data(), nl * nw * 4, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     ctx->have_reset = 1;
     return MRP_OK;
@@ -525,16 +565,20 @@ int mrp_debug_velbench(int device, int nc, int pcount, int iters, int blocks, ui
 
 // Diagnostic builds only: read-and-clear one stamp symbol of every env unit, combined by sum
 // (or max); only the units whose kernels ran hold non-zero values.
+// A variant library (build.py --variant ... -DMRP_STAMPS) instruments only the env units it lists;
+// units without the stamps are skipped, and a library with none answers MRP_E_STATE.
 static int debug_combine(int what, uint64_t* out, size_t n, bool take_max) {
     std::vector<uint64_t> tmp(n);
     for (size_t k = 0; k < n; ++k) out[k] = 0;
+    int have = 0;
     for (int i = 0; i < N_ENVS; ++i) {
         hipError_t e = env_ops(i)->debug_read(what, tmp.data(), n * sizeof(uint64_t));
-        if (e == hipErrorNotSupported) return MRP_E_STATE;
+        if (e == hipErrorNotSupported) continue;
         if (e != hipSuccess) return MRP_E_HIP;
+        ++have;
         for (size_t k = 0; k < n; ++k) out[k] = take_max ? std::max(out[k], tmp[k]) : out[k] + tmp[k];
     }
-    return MRP_OK;
+    return have ? MRP_OK : MRP_E_STATE;
 }
 
 int mrp_debug_stamps(int device, uint64_t* out16) {
@@ -557,13 +601,15 @@ int mrp_debug_trace(int device, uint32_t* out, int n_lanes) {
     if (!out || n_lanes <= 0 || n_lanes > 16384 || hipSetDevice(device) != hipSuccess) return MRP_E_ARG;
     std::vector<uint32_t> tmp((size_t)n_lanes * 24);
     std::memset(out, 0, tmp.size() * 4);
+    int have = 0;
     for (int i = 0; i < N_ENVS; ++i) {   // only the unit that stepped has a non-zero trace
         hipError_t e = env_ops(i)->debug_read(DBG_TRACE, tmp.data(), tmp.size() * 4);
-        if (e == hipErrorNotSupported) return MRP_E_STATE;
+        if (e == hipErrorNotSupported) continue;
         if (e != hipSuccess) return MRP_E_HIP;
+        ++have;
         for (size_t k = 0; k < tmp.size(); ++k) out[k] |= tmp[k];
     }
-    return MRP_OK;
+    return have ? MRP_OK : MRP_E_STATE;
 }
 
 

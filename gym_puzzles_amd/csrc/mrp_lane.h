@@ -414,8 +414,10 @@ struct Launch {
     }
     static constexpr EnvOps ops() {
         using D = Dims<ENV>;
-        return EnvOps{lane_words<ENV>(), (int)(offsetof(LaneState<ENV>, toiEvents) / 4),
-                      {D::OBS, D::ACT, D::NDRAW, D::NA, D::NB, D::NF}, upload_tables, init, reset, step,
+        using LS = LaneState<ENV>;
+        return EnvOps{lane_words<ENV>(), (int)(offsetof(LS, toiEvents) / 4),
+                      {D::OBS, D::ACT, D::NDRAW, D::NA, D::NB, D::NF},
+                      StateIO<ENV>::P, LS::C, LS::NCA, StateIO<ENV>::HWW, upload_tables, init, reset, step,
                       bodies, faults, counters, render, goals, debug_read, debug_progress};
     }
 };

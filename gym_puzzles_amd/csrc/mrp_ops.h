@@ -59,6 +59,9 @@ struct EnvOps {
     int words;                 // lane_words<ENV>()
     int counters_word;         // word offset of LaneState::toiEvents (followed by posIters)
     int dims[6];               // Dims<ENV>: OBS, ACT, NDRAW, NA, NB, NF (mrp_create checks them against the tables)
+    // contact-slot layout of LaneState (mrp_set_state repairs an understated high-water mark cHW):
+    // word offset of cnext (the first of `cslot_arrays` contiguous arrays of `cslot_n` words) and of cHW
+    int cslot_word, cslot_n, cslot_arrays, chw_word;
     hipError_t (*upload_tables)(const EnvTables* all);   // all N_ENVS tables -> this unit's __constant__ copy
     void (*init)(hipStream_t, uint32_t* state, int nl);
     void (*reset)(hipStream_t, uint32_t* state, int nl, const uint8_t* mask, const double* draws, const float* actions,

@@ -1,4 +1,4 @@
-// mrp_world.h -- one MultiRobotPuzzle world ("lane") stepped by one GPU thread.
+// mrp_world.h -- one MultiRobotPuzzle world ("lane") stepped by one wavefront.
 //
 // This is the MI355X-native restatement of the per-timestep path of
 // gym_puzzles/envs/multi_robot_puzzle_00.py:413-521 (v0) and multi_robot_puzzle_02.py:444-584
@@ -6,10 +6,16 @@
 // sequential-impulse contact solver with the 2-point block solver, position solver, TOI),
 // then contact flags, distances, observation, reward, done.
 //
-// Layout: the persistent lane state (LaneState<ENV>) is a POD of 32-bit words stored
-// structure-of-arrays across lanes in HBM (word w of lane l at base[w * n_lanes + l]), so
-// the wave's 64 lanes read/write each word coalesced.  Inside a step the thread works on a
-// private copy; per-step temporaries (islands, constraints) are private arrays.
+// Execution model: one 64-thread workgroup (one wave) owns one lane for a whole k_step.  The
+// lane's persistent state (LaneState<ENV>, a POD of 32-bit words) is stored lane-major in HBM --
+// each lane one contiguous block, moved by the wave as coalesced 16-B granules (mrp_lane.h
+// StateIO) -- and lives in LDS (Shared<ENV>) for the step.  Thread 0 runs the order-sensitive
+// serial parts (tree updates, sorted AddPair, contact commit and events, island DFS and set-up,
+// TOI bookkeeping); all 64 threads run the data-parallel parts (pair tests, one contact's SAT per
+// thread, TOI candidate scans, state I/O); the velocity and position iterations run on the whole
+// wave with the island in registers (one or two contacts: every thread evaluates the same update)
+// or spread across the wave (larger islands: contact i's constants in thread i, body k's state in
+// thread k, one contact update after the other through v_readlane / v_writelane).
 //
 // Box2D's pointer-linked lists become index lists: the world contact list is a doubly
 // linked list of slots in creation-descending order, and a body's contact-edge list is the

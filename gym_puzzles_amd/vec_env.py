@@ -64,7 +64,14 @@ class MultiRobotPuzzleVecEnv(_VecEnvBase):
         self.device = device
         self._seed = seed
         self._lane_offset = lane_offset
-        self.frameskip = int(frameskip)   # MultiRobotPuzzle2(frameskip=k): world.Step calls per env step
+        # MultiRobotPuzzle2(frameskip=k) (multi_robot_puzzle_02.py:139,476-478): world.Step calls per env
+        # step.  Only the v2 classes take it: v0 fixes frameskip 1 for its low-dim observations
+        # (multi_robot_puzzle_00.py:161-162) and RobotPuzzleBase has none (core.py:77-418)
+        self.frameskip = int(frameskip)
+        if self.frameskip < 1:
+            raise ValueError("frameskip must be >= 1")
+        if self.frameskip != 1 and ENV_CFG[self.env_index][0] != 2:
+            raise ValueError(f"frameskip={frameskip}: only the MultiRobotPuzzle2 envs (v2) repeat world.Step per env step")
         self.observation_space = make_box(-np.inf, np.inf, shape=(d["obs_dim"],), dtype=np.float32)
         self.action_space = make_box(-1.0, 1.0, shape=(d["act_dim"],), dtype=np.float32)
         self.max_episode_steps = d["max_episode_steps"] if max_episode_steps is None else max_episode_steps

@@ -1400,6 +1400,52 @@ void b2o_topo_diag(int on, long* sig64, long* w64) {
     if (on >= 0) { g_topo_diag = on; for (int k = 0; k < 64; ++k) { g_topo_sig[k] = 0; g_topo_w[k] = 0; } }
 }
 
+#ifdef OR_NO_WORK
+/* CPU-baseline builds (Makefile targets `fast` and `early`, bench.py cpu_baseline): the velocity
+ * sweeps without the work model.  OR_EARLY_EXIT stops at the device's exact early exit
+ * (mrp_world.h solver_velocity_*): a snapshot two sweeps before every sweep k with 180 - k = 0
+ * (mod 4), and once the state after k equals it the state has period 1 or 2, so the state after
+ * all `iters` sweeps is the state after k -- the same bits, fewer sweeps.  Without OR_EARLY_EXIT
+ * all `iters` sweeps run, as b2ContactSolver::SolveVelocityConstraints is called by b2Island::Solve. */
+static void velocity_sweeps(Solver* s, int iters, int nbodies) {
+#ifdef OR_EARLY_EXIT
+    const int nc = s->count, ns = 4 * nc + 3 * nbodies;
+    float snap_st[512], cur_st[512];
+    float* snap = ns <= 512 ? snap_st : (float*)malloc(sizeof(float) * (size_t)ns);
+    float* cur = ns <= 512 ? cur_st : (float*)malloc(sizeof(float) * (size_t)ns);
+#define SWEEP_STATE(dst) do {                                                                      \
+        int k_ = 0;                                                                                \
+        for (int i_ = 0; i_ < nc; ++i_)                                                            \
+            for (int j_ = 0; j_ < 2; ++j_) {                                                       \
+                (dst)[k_++] = s->vcs[i_].points[j_].normalImpulse;                                 \
+                (dst)[k_++] = s->vcs[i_].points[j_].tangentImpulse;                                \
+            }                                                                                      \
+        for (int b_ = 0; b_ < nbodies; ++b_) {                                                     \
+            (dst)[k_++] = s->velocities[b_].v.x; (dst)[k_++] = s->velocities[b_].v.y;              \
+            (dst)[k_++] = s->velocities[b_].w;                                                     \
+        }                                                                                          \
+    } while (0)
+    int have = (iters & 3) == 2;
+    if (have) SWEEP_STATE(snap);
+    for (int it = 0; it < iters; ++it) {
+        solver_solve_velocity(s);
+        const int left = iters - (it + 1);
+        if ((left & 3) == 0 && have) {
+            SWEEP_STATE(cur);
+            if (memcmp(cur, snap, sizeof(float) * (size_t)ns) == 0) break;
+        }
+        if ((left & 3) == 2) { SWEEP_STATE(snap); have = 1; }
+    }
+#undef SWEEP_STATE
+    if (snap != snap_st) free(snap);
+    if (cur != cur_st) free(cur);
+#else
+    (void)nbodies;
+    for (int it = 0; it < iters; ++it) solver_solve_velocity(s);
+#endif
+}
+#endif
+
 static void island_solve(Island* is, World* w, TimeStep step) {
     float h = step.dt;
     for (int i = 0; i < is->bodyCount; ++i) {
@@ -1422,6 +1468,15 @@ static void island_solve(Island* is, World* w, TimeStep step) {
     solver_init(&s, step, is->contacts, is->contactCount, is->positions, is->velocities);
     solver_init_velocity_constraints(&s);
     if (step.warmStarting) solver_warm_start(&s);
+#ifdef OR_NO_WORK
+    velocity_sweeps(&s, step.velocityIterations, is->bodyCount);
+    solver_store_impulses(&s);
+    integrate_positions(is, h, 0);
+    for (int i = 0; i < step.positionIterations; ++i) {
+        w->posIters++;
+        if (solver_solve_position(&s, 0, -1, -1)) break;
+    }
+#else
     const int sweeps = work_velocity_sweeps(&s, step.velocityIterations, is->bodyCount);
     w->velIters += (long)step.velocityIterations * is->contactCount;
     solver_store_impulses(&s);
@@ -1449,6 +1504,7 @@ static void island_solve(Island* is, World* w, TimeStep step) {
         w->stepIslSum += units;
         if (units > w->stepIslMax) w->stepIslMax = units;
     }
+#endif
     for (int i = 0; i < is->bodyCount; ++i) {
         Body* body = is->bodies[i];
         body->sweep.c = is->positions[i].c; body->sweep.a = is->positions[i].a;
@@ -1466,6 +1522,17 @@ static void island_solve_toi(Island* is, TimeStep sub, int toiIndexA, int toiInd
     }
     Solver s;
     solver_init(&s, sub, is->contacts, is->contactCount, is->positions, is->velocities);
+#ifdef OR_NO_WORK
+    (void)k;
+    for (int i = 0; i < sub.positionIterations; ++i)
+        if (solver_solve_position(&s, 1, toiIndexA, toiIndexB)) break;
+    is->bodies[toiIndexA]->sweep.c0 = is->positions[toiIndexA].c;
+    is->bodies[toiIndexA]->sweep.a0 = is->positions[toiIndexA].a;
+    is->bodies[toiIndexB]->sweep.c0 = is->positions[toiIndexB].c;
+    is->bodies[toiIndexB]->sweep.a0 = is->positions[toiIndexB].a;
+    solver_init_velocity_constraints(&s);
+    velocity_sweeps(&s, sub.velocityIterations, is->bodyCount);
+#else
     int passes = 0;
     for (int i = 0; i < sub.positionIterations; ++i) {
         ++passes;
@@ -1492,6 +1559,7 @@ static void island_solve_toi(Island* is, TimeStep sub, int toiIndexA, int toiInd
         k->toi_vel_upd += (long)sweeps * s.count; k->toi_vel_levels += (long)sweeps * L;
         k->vel_pipe += work_pipe(&s, dyn, sweeps, 0);
     }
+#endif
     integrate_positions(is, sub.dt, 1);
     solver_free(&s);
 }

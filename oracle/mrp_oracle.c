@@ -738,35 +738,55 @@ int or_body_mass(const OrEnv* e, int i, float* out4) {
  * max_steps <= 0 uses the registered TimeLimit.  bodies [n_lanes][6*(n_blocks+n_agents)] final state, rsum [n_lanes] summed float32(reward),
  * resets [n_lanes] episodes started. */
 #include <omp.h>
-static long batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_t lane_offset, const double* lo,
+static long batch_run(int env_id, int n_lanes, int skip, int steps, uint64_t seed, uint64_t lane_offset, const double* lo,
                       const double* hi, int max_steps, int threads, double* seconds, float* bodies, double* rsum,
                       int* resets, int* caps, long* work);
 long or_batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_t lane_offset, const double* lo,
                   const double* hi, int max_steps, int threads, double* seconds, float* bodies, double* rsum,
                   int* resets) {
-    return batch_run(env_id, n_lanes, steps, seed, lane_offset, lo, hi, max_steps, threads, seconds, bodies, rsum, resets,
+    return batch_run(env_id, n_lanes, 0, steps, seed, lane_offset, lo, hi, max_steps, threads, seconds, bodies, rsum, resets,
+                     NULL, NULL);
+}
+/* or_batch_run with `skip` untimed steps first: *seconds times only steps skip+1 .. skip+steps of
+ * every lane (bench.py's CPU baseline on the GPU line's step window); returns the timed env-steps */
+long or_batch_run_window(int env_id, int n_lanes, int skip, int steps, uint64_t seed, uint64_t lane_offset, const double* lo,
+                         const double* hi, int max_steps, int threads, double* seconds, float* bodies, double* rsum,
+                         int* resets) {
+    return batch_run(env_id, n_lanes, skip, steps, seed, lane_offset, lo, hi, max_steps, threads, seconds, bodies, rsum, resets,
                      NULL, NULL);
 }
 long or_batch_capacity(int env_id, int n_lanes, int steps, uint64_t seed, const double* lo, const double* hi, int max_steps,
                        int threads, int* caps8) {
     double sec;
     for (int k = 0; k < 8; ++k) caps8[k] = 0;
-    return batch_run(env_id, n_lanes, steps, seed, 0, lo, hi, max_steps, threads, &sec, NULL, NULL, NULL, caps8, NULL);
+    return batch_run(env_id, n_lanes, 0, steps, seed, 0, lo, hi, max_steps, threads, &sec, NULL, NULL, NULL, caps8, NULL);
 }
 long or_batch_work(int env_id, int n_lanes, int steps, uint64_t seed, const double* lo, const double* hi, int max_steps,
                    int threads, long* work) {
     double sec;
-    return batch_run(env_id, n_lanes, steps, seed, 0, lo, hi, max_steps, threads, &sec, NULL, NULL, NULL, NULL, work);
+    return batch_run(env_id, n_lanes, 0, steps, seed, 0, lo, hi, max_steps, threads, &sec, NULL, NULL, NULL, NULL, work);
 }
-static long batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_t lane_offset, const double* lo,
+/* the build's name for the solver variant it was compiled as (bench.py records it) */
+const char* or_build_kind(void) {
+#if defined(OR_NO_WORK) && defined(OR_EARLY_EXIT)
+    return "early-exit port: work model compiled out, velocity sweeps stop at the device's exact period-1/2 exit";
+#elif defined(OR_NO_WORK)
+    return "port: work model compiled out, all 180 velocity sweeps (b2Island::Solve)";
+#else
+    return "checker: work model compiled in";
+#endif
+}
+static long batch_run(int env_id, int n_lanes, int skip, int steps, uint64_t seed, uint64_t lane_offset, const double* lo,
                       const double* hi, int max_steps, int threads, double* seconds, float* bodies, double* rsum,
                       int* resets, int* caps, long* work) {
-    if (!valid(env_id) || n_lanes <= 0 || steps < 0) return -1;
+    if (!valid(env_id) || n_lanes <= 0 || steps < 0 || skip < 0) return -1;
     const Cfg cfg = CFGS[env_id];
     const int limit = max_steps > 0 ? max_steps : cfg.max_steps;
     const int nbody = 6 * (cfg.n_blocks + cfg.n_agents);
     OrEnv** envs = (OrEnv**)calloc((size_t)n_lanes, sizeof(OrEnv*));
     int* episode = (int*)calloc((size_t)n_lanes, sizeof(int));
+    int* elapsed = (int*)calloc((size_t)n_lanes, sizeof(int));
+    double* rs = (double*)calloc((size_t)n_lanes, sizeof(double));
     if (threads > 0) omp_set_num_threads(threads);
     double t0 = 0.0, t1 = 0.0;
     long total = 0;
@@ -782,43 +802,50 @@ static long batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_
             or_reset(envs[l], draws, act, obs);
             episode[l] = 1;
         }
+        /* phase 0: the untimed steps [0, skip); phase 1: the timed steps [skip, skip + steps) */
+        for (int phase = 0; phase < 2; ++phase) {
+            const int s0 = phase ? skip : 0, s1 = phase ? skip + steps : skip;
+            if (s1 <= s0) continue;
+#pragma omp barrier
 #pragma omp single
-        t0 = omp_get_wtime();
-        /* dynamic: a lane's cost varies by orders of magnitude between steps (contact islands), and
-         * lanes are independent, so the CPU baseline takes the best balance it can */
+            t0 = omp_get_wtime();
+            /* dynamic: a lane's cost varies by orders of magnitude between steps (contact islands), and
+             * lanes are independent, so the CPU baseline takes the best balance it can */
 #pragma omp for schedule(dynamic, 4) reduction(+:total)
-        for (int l = 0; l < n_lanes; ++l) {
-            OrEnv* e = envs[l];
-            const uint64_t g = lane_offset + (uint64_t)l;
-            int elapsed = 0;
-            double rs = 0.0;
-            for (int s = 0; s < steps; ++s) {
-                for (int j = 0; j < cfg.act_dim; ++j)
-                    act[j] = (float)(-1.0 + 2.0 * or_rng_u01(seed, g, 3, (uint64_t)s * 64 + (uint64_t)j));
-                long w0[20];
-                if (work) or_work(e, w0);
-                or_step(e, act, obs, &rew, &done, &kind);
-                rs += (double)(float)rew;
-                ++total;
-                if (done || ++elapsed >= limit) {
-                    const uint64_t ctr = (uint64_t)episode[l] * 64;
-                    for (int d = 0; d < cfg.n_draws; ++d)
-                        draws[d] = lo[d] + (hi[d] - lo[d]) * or_rng_u01(seed, g, 1, ctr + (uint64_t)d);
-                    for (int j = 0; j < cfg.act_dim; ++j) act[j] = (float)(-1.0 + 2.0 * or_rng_u01(seed, g, 2, ctr + (uint64_t)j));
-                    or_reset(e, draws, act, obs);
-                    ++episode[l];
-                    elapsed = 0;
-                }
-                if (work) {   /* this launch's work for the lane: the step plus an auto-reset's own step */
-                    long w1[20];
-                    or_work(e, w1);
-                    for (int k = 0; k < 20; ++k) work[((size_t)s * n_lanes + l) * 20 + k] = w1[k] - w0[k];
+            for (int l = 0; l < n_lanes; ++l) {
+                OrEnv* e = envs[l];
+                const uint64_t g = lane_offset + (uint64_t)l;
+                for (int s = s0; s < s1; ++s) {
+                    for (int j = 0; j < cfg.act_dim; ++j)
+                        act[j] = (float)(-1.0 + 2.0 * or_rng_u01(seed, g, 3, (uint64_t)s * 64 + (uint64_t)j));
+                    long w0[20];
+                    if (work) or_work(e, w0);
+                    or_step(e, act, obs, &rew, &done, &kind);
+                    rs[l] += (double)(float)rew;
+                    if (phase) ++total;
+                    if (done || ++elapsed[l] >= limit) {
+                        const uint64_t ctr = (uint64_t)episode[l] * 64;
+                        for (int d = 0; d < cfg.n_draws; ++d)
+                            draws[d] = lo[d] + (hi[d] - lo[d]) * or_rng_u01(seed, g, 1, ctr + (uint64_t)d);
+                        for (int j = 0; j < cfg.act_dim; ++j)
+                            act[j] = (float)(-1.0 + 2.0 * or_rng_u01(seed, g, 2, ctr + (uint64_t)j));
+                        or_reset(e, draws, act, obs);
+                        ++episode[l];
+                        elapsed[l] = 0;
+                    }
+                    if (work) {   /* this launch's work for the lane: the step plus an auto-reset's own step */
+                        long w1[20];
+                        or_work(e, w1);
+                        for (int k = 0; k < 20; ++k) work[((size_t)s * n_lanes + l) * 20 + k] = w1[k] - w0[k];
+                    }
                 }
             }
-            if (rsum) rsum[l] = rs;
-        }
 #pragma omp single
-        t1 = omp_get_wtime();
+            t1 = omp_get_wtime();
+        }
+#pragma omp for schedule(static)
+        for (int l = 0; l < n_lanes; ++l)
+            if (rsum) rsum[l] = rs[l];
 #pragma omp for schedule(static)
         for (int l = 0; l < n_lanes; ++l) {
             if (bodies) or_get_bodies(envs[l], bodies + (size_t)l * nbody);
@@ -833,6 +860,6 @@ static long batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_
         }
     }
     *seconds = t1 - t0;
-    free(envs); free(episode);
+    free(envs); free(episode); free(elapsed); free(rs);
     return total;
 }

@@ -51,6 +51,13 @@ int or_body_mass(const OrEnv* e, int i, float* out4);
 long or_batch_run(int env_id, int n_lanes, int steps, uint64_t seed, uint64_t lane_offset, const double* lo,
                   const double* hi, int max_steps, int threads, double* seconds, float* bodies, double* rsum,
                   int* resets);
+/* or_batch_run with `skip` untimed steps first; *seconds and the return value cover only the
+ * `steps` steps after them (the CPU baseline on the GPU line's window) */
+long or_batch_run_window(int env_id, int n_lanes, int skip, int steps, uint64_t seed, uint64_t lane_offset, const double* lo,
+                         const double* hi, int max_steps, int threads, double* seconds, float* bodies, double* rsum,
+                         int* resets);
+/* which solver variant this library was built as (checker / port / early-exit port; oracle/Makefile) */
+const char* or_build_kind(void);
 
 /* capacity high-water marks of one lane since creation: max live contacts, max tree node id,
  * max move-buffer fill, max island bodies / contacts, max TOI-island bodies / contacts, tree node

@@ -18,7 +18,13 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "libmrp_oracle.so")
+# solver variants of the same sources (oracle/Makefile): the checker carries the work model; the
+# CPU baseline of bench.py times "port" (all 180 velocity sweeps, as b2Island::Solve runs them) and
+# "early" (the device's exact period-1/2 early exit of the sweeps); all three give the same bits
+VARIANTS = {"checker": _LIB_PATH, "port": os.path.join(_HERE, "build", "libmrp_oracle_port.so"),
+            "early": os.path.join(_HERE, "build", "libmrp_oracle_early.so")}
 _lib = None
+_variants = {}
 
 ENV_IDS = {
     "MultiRobotPuzzle-v0": 0,
@@ -45,53 +51,68 @@ def build() -> str:
     return _LIB_PATH
 
 
-def lib():
+def lib(variant: str = "checker"):
     global _lib
+    if variant != "checker":
+        if variant not in _variants:
+            if not os.path.exists(VARIANTS[variant]):
+                build()
+            _variants[variant] = _bind(ctypes.CDLL(VARIANTS[variant]))
+        return _variants[variant]
     if _lib is None:
         if not os.path.exists(_LIB_PATH):
             build()
-        L = ctypes.CDLL(_LIB_PATH)
-        c_int, c_float, c_double = ctypes.c_int, ctypes.c_float, ctypes.c_double
-        P = ctypes.c_void_p
-        for name in ("or_obs_dim", "or_act_dim", "or_n_draws", "or_n_agents", "or_n_blocks", "or_max_episode_steps"):
-            getattr(L, name).argtypes = [c_int]
-            getattr(L, name).restype = c_int
-        L.or_create.argtypes = [c_int]
-        L.or_create.restype = P
-        L.or_destroy.argtypes = [P]
-        L.or_reset.argtypes = [P, P, P, P]
-        L.or_step.argtypes = [P, P, P, P, P, P]
-        L.or_set_shaped.argtypes = [P, c_double, c_double, c_double]
-        L.or_set_frameskip.argtypes = [P, c_int]
-        L.or_get_bodies.argtypes = [P, P]
-        L.or_get_bodies.restype = c_int
-        L.or_get_flags.argtypes = [P, P, P]
-        L.or_contact_count.argtypes = [P]
-        L.or_contact_count.restype = c_int
-        L.or_counters.argtypes = [P, P, P]
-        L.or_counters_ex.argtypes = [P, P]
-        L.or_proxy_ids.argtypes = [P, P]
-        L.or_proxy_ids.restype = c_int
-        L.or_sinf.argtypes = [c_float]
-        L.or_sinf.restype = c_float
-        L.or_cosf.argtypes = [c_float]
-        L.or_cosf.restype = c_float
-        L.or_sincos_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-        L.or_sincos_batch.restype = None
-        L.or_rng_u01.argtypes = [ctypes.c_uint64] * 4
-        L.or_rng_u01.restype = c_double
-        L.or_body_mass.argtypes = [P, c_int, P]
-        L.or_body_mass.restype = c_int
-        L.or_batch_run.argtypes = [c_int, c_int, c_int, ctypes.c_uint64, ctypes.c_uint64, P, P, c_int, c_int, P, P, P, P]
-        L.or_batch_run.restype = ctypes.c_long
-        L.or_batch_capacity.argtypes = [c_int, c_int, c_int, ctypes.c_uint64, P, P, c_int, c_int, P]
-        L.or_batch_capacity.restype = ctypes.c_long
-        L.or_capacity.argtypes = [P, P]
-        L.or_work.argtypes = [P, P]
-        L.or_batch_work.argtypes = [c_int, c_int, c_int, ctypes.c_uint64, P, P, c_int, c_int, P]
-        L.or_batch_work.restype = ctypes.c_long
-        _lib = L
+        _lib = _bind(ctypes.CDLL(_LIB_PATH))
     return _lib
+
+
+def _bind(L):
+    """Declare the argument / return types of the oracle's entry points on a loaded build."""
+    c_int, c_float, c_double = ctypes.c_int, ctypes.c_float, ctypes.c_double
+    P = ctypes.c_void_p
+    for name in ("or_obs_dim", "or_act_dim", "or_n_draws", "or_n_agents", "or_n_blocks", "or_max_episode_steps"):
+        getattr(L, name).argtypes = [c_int]
+        getattr(L, name).restype = c_int
+    L.or_create.argtypes = [c_int]
+    L.or_create.restype = P
+    L.or_destroy.argtypes = [P]
+    L.or_reset.argtypes = [P, P, P, P]
+    L.or_step.argtypes = [P, P, P, P, P, P]
+    L.or_set_shaped.argtypes = [P, c_double, c_double, c_double]
+    L.or_set_frameskip.argtypes = [P, c_int]
+    L.or_get_bodies.argtypes = [P, P]
+    L.or_get_bodies.restype = c_int
+    L.or_get_flags.argtypes = [P, P, P]
+    L.or_contact_count.argtypes = [P]
+    L.or_contact_count.restype = c_int
+    L.or_counters.argtypes = [P, P, P]
+    L.or_counters_ex.argtypes = [P, P]
+    L.or_proxy_ids.argtypes = [P, P]
+    L.or_proxy_ids.restype = c_int
+    L.or_sinf.argtypes = [c_float]
+    L.or_sinf.restype = c_float
+    L.or_cosf.argtypes = [c_float]
+    L.or_cosf.restype = c_float
+    L.or_sincos_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    L.or_sincos_batch.restype = None
+    L.or_rng_u01.argtypes = [ctypes.c_uint64] * 4
+    L.or_rng_u01.restype = c_double
+    L.or_body_mass.argtypes = [P, c_int, P]
+    L.or_body_mass.restype = c_int
+    L.or_batch_run.argtypes = [c_int, c_int, c_int, ctypes.c_uint64, ctypes.c_uint64, P, P, c_int, c_int, P, P, P, P]
+    L.or_batch_run.restype = ctypes.c_long
+    L.or_batch_capacity.argtypes = [c_int, c_int, c_int, ctypes.c_uint64, P, P, c_int, c_int, P]
+    L.or_batch_capacity.restype = ctypes.c_long
+    L.or_capacity.argtypes = [P, P]
+    L.or_work.argtypes = [P, P]
+    L.or_batch_work.argtypes = [c_int, c_int, c_int, ctypes.c_uint64, P, P, c_int, c_int, P]
+    L.or_batch_work.restype = ctypes.c_long
+    L.or_batch_run_window.argtypes = [c_int, c_int, c_int, c_int, ctypes.c_uint64, ctypes.c_uint64, P, P, c_int, c_int,
+                                      P, P, P, P]
+    L.or_batch_run_window.restype = ctypes.c_long
+    L.or_build_kind.argtypes = []
+    L.or_build_kind.restype = ctypes.c_char_p
+    return L
 
 
 def _ptr(a: np.ndarray):
@@ -179,27 +200,32 @@ class OracleEnv:
         return out[:n].copy()
 
 
+def build_kind(variant: str = "checker") -> str:
+    return lib(variant).or_build_kind().decode()
+
+
 def rng_u01(seed: int, lane: int, stream: int, counter: int) -> float:
     return lib().or_rng_u01(seed, lane, stream, counter)
 
 
 def batch_run(env_id: int, lanes: int, steps: int, seed: int, bounds, threads: int = 1, lane_offset: int = 0,
-              outputs: bool = False, max_steps: int = 0):
-    """Run `lanes` oracle envs for `steps` steps each with the device path's synthetic inputs
-    (counter RNG actions and spawns, auto-reset; see or_batch_run) on `threads` OpenMP threads.
+              outputs: bool = False, max_steps: int = 0, skip: int = 0, variant: str = "checker"):
+    """Run `lanes` oracle envs for `skip` + `steps` steps each with the device path's synthetic
+    inputs (counter RNG actions and spawns, auto-reset; see or_batch_run) on `threads` OpenMP
+    threads; only the last `steps` are timed and counted.  `variant` picks the build (VARIANTS).
     Returns (env_steps, seconds) or, with outputs=True, (env_steps, seconds, bodies, reward_sums,
     episodes)."""
     lo = np.ascontiguousarray([b[0] for b in bounds], dtype=np.float64)
     hi = np.ascontiguousarray([b[1] for b in bounds], dtype=np.float64)
     sec = np.zeros(1, np.float64)
-    L = lib()
+    L = lib(variant)
     nb = 6 * (L.or_n_agents(env_id) + L.or_n_blocks(env_id))
     bodies = np.zeros((lanes, nb), np.float32) if outputs else None
     rsum = np.zeros(lanes, np.float64) if outputs else None
     eps = np.zeros(lanes, np.int32) if outputs else None
     P = lambda a: None if a is None else _ptr(a)  # noqa: E731
-    n = L.or_batch_run(env_id, lanes, steps, seed, lane_offset, _ptr(lo), _ptr(hi), max_steps, threads, _ptr(sec),
-                       P(bodies), P(rsum), P(eps))
+    n = L.or_batch_run_window(env_id, lanes, skip, steps, seed, lane_offset, _ptr(lo), _ptr(hi), max_steps, threads,
+                              _ptr(sec), P(bodies), P(rsum), P(eps))
     if n < 0:
         raise ValueError("or_batch_run: bad arguments")
     if outputs:

@@ -474,3 +474,73 @@ def test_frameskip_parity(gpu_lib, orc, env_id, frameskip):
                 _eq(f"reset obs@{t}", o2[l], envs[l].reset(d2[l], a2[l]).astype(np.float32))
     assert b.counters()[1] == sum(o.counters()[1] for o in envs)
     b.close()
+
+
+def test_set_state_repairs_understated_contact_mark(gpu_lib):
+    """k_step moves only the contact slots below LaneState::cHW; a state injected through
+    mrp_set_state with that mark understated (here zeroed on every lane) must not lose its live
+    contacts: mrp_set_state recomputes the mark from the slots, so the lanes step exactly as from
+    the unmodified state."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from lane_layout import offsets
+    a, b = _twin(0, 64, seed=41, warm=40)
+    snap = a.get_state().copy()
+    off, _ = offsets(0)
+    assert (snap[:, off["cHW"]] > 0).any(), "no lane holds a contact slot: the test needs a live contact"
+    bad = snap.copy()
+    bad[:, off["cHW"]] = 0
+    a.set_state(snap)
+    b.set_state(bad)
+    assert (b.get_state()[:, off["cHW"]].astype(np.int32) >= 1)[snap[:, off["cHW"]] > 0].all()
+    for t in range(30):
+        oa, ra, da, _ = a.step()
+        ob, rb, db, _ = b.step()
+        _eq(f"obs@{t}", ob, oa)
+        _eq(f"reward@{t}", rb, ra)
+    _eq("bodies", b.bodies(), a.bodies())
+
+
+@pytest.mark.parametrize("env_id", [2, 4])
+def test_eight_shard_composition_equals_one_batch(gpu_lib, env_id):
+    """BASELINE.json configs[3]/[4]: 8192 global lanes as 8 shards of 1024 (rank r owns lane_offset
+    r * 1024, gym_puzzles_amd/dist.py), each stepped by its own libmrp ctx on the device path and packed
+    into the per-step message with StepGather.pack; the 8 packed blocks, in rank order, equal one
+    8192-lane batch's packed outputs bit for bit at every step (obs, reward, done), across auto-resets."""
+    import torch
+
+    from gym_puzzles_amd import Batch
+    from gym_puzzles_amd.dist import Shard, StepGather
+    L, R, steps = 1024, 8, 60
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    full = Batch(env_id, L * R, seed=13)
+    shards = [Batch(env_id, L, seed=13, lane_offset=r * L) for r in range(R)]
+    for b in [full] + shards:
+        b.set_stream(stream)          # the packing runs on torch's stream: same stream, ordered
+        b.set_auto_reset(True)
+        b.set_time_limit(25)
+        b.reset()
+    O = full.obs_dim
+
+    def outs(n):
+        return (torch.zeros((n, O), dtype=torch.float32, device=dev), torch.zeros(n, dtype=torch.float32, device=dev),
+                torch.zeros(n, dtype=torch.uint8, device=dev))
+    fo = outs(L * R)
+    so = [outs(L) for _ in range(R)]
+    gfull = StepGather(Shard(0, 1, L * R), O, dev)
+    gsh = [StepGather(Shard(r, R, L), O, dev) for r in range(R)]
+    n_done = 0
+    for t in range(steps):
+        full.step_device(0, fo[0].data_ptr(), fo[1].data_ptr(), fo[2].data_ptr())
+        for b, o in zip(shards, so):
+            b.step_device(0, o[0].data_ptr(), o[1].data_ptr(), o[2].data_ptr())
+        want = gfull.pack(*fo)
+        got = torch.cat([g.pack(*o) for g, o in zip(gsh, so)])
+        assert torch.equal(got.view(torch.int32), want.view(torch.int32)), f"packed step {t} differs"
+        n_done += int(fo[2].sum().item())
+    assert n_done >= L * R, "every lane should have auto-reset at least once (TimeLimit 25)"
+    _eq("bodies", np.concatenate([b.bodies() for b in shards]), full.bodies())
+    for b in [full] + shards:
+        assert not b.faults().any()
+        b.close()

@@ -414,3 +414,30 @@ def test_work_model_is_consistent(oracle_lib):
         table = json.load(f)
     for key in ("0:4096:6:25:17", "0:4096:21:220:17"):
         assert table[key]["flops_per_launch"] > 0 and table[key]["latency_floor_ms"] > 0
+
+
+@pytest.mark.parametrize("env_id", [0, 1, 2, 4, 5])
+def test_baseline_builds_bit_identical(orc, env_id):
+    """bench.py's CPU baseline times two builds of the oracle without the work model (oracle/Makefile:
+    `port`, all 180 velocity sweeps; `early`, the device's exact period-1/2 early exit).  Both must
+    produce the checker's bits: final body state, per-lane reward sums and episode counts over a
+    window that starts after untimed steps (or_batch_run_window) and crosses auto-resets."""
+    lanes, skip, steps = 48, 5, 40
+    ref = orc.batch_run(env_id, lanes, steps, 17, draw_bounds(env_id), threads=4, outputs=True, skip=skip, max_steps=25)
+    for variant in ("port", "early"):
+        got = orc.batch_run(env_id, lanes, steps, 17, draw_bounds(env_id), threads=4, outputs=True, skip=skip, max_steps=25,
+                            variant=variant)
+        assert got[0] == ref[0] == lanes * steps   # only the timed steps are counted
+        for name, x, y in zip(("bodies", "reward sums", "episodes"), got[2:], ref[2:]):
+            assert np.array_equal(x, y), f"{variant}: {name} differ from the checker build"
+    assert "port" in orc.build_kind("port") and "early-exit" in orc.build_kind("early")
+
+
+def test_batch_run_window_equals_unsplit_run(orc):
+    """Untimed steps followed by timed steps (or_batch_run_window) advance every lane exactly like one
+    run over both: the split only moves the clock."""
+    a = orc.batch_run(2, 32, 30, 9, draw_bounds(2), threads=4, outputs=True, skip=10)
+    b = orc.batch_run(2, 32, 40, 9, draw_bounds(2), threads=4, outputs=True)
+    assert a[0] == 32 * 30 and b[0] == 32 * 40
+    for x, y in zip(a[2:], b[2:]):
+        assert np.array_equal(x, y)
