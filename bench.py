@@ -161,26 +161,49 @@ def single_env_rate(env_id: int, steps: int = 300) -> dict:
                     "1-lane kernel, actions and outputs through the ctx's pinned host buffer"}
 
 
-def load_valu_latency(env_id: int, lanes: int, first: int, last: int, seed: int, kern_ms: float):
-    """roofline.valu / roofline.latency: the oracle op-count model of exactly this workload
-    (tools/roofline_model.py -> profiles/r3_valu_latency.json, keyed by env, lanes, timed step
-    window and seed) over the live kernel_ms; None when the table has no entry for this run."""
+def load_valu(env_id: int, lanes: int, first: int, last: int, seed: int, kern_ms: float):
+    """roofline.valu: the oracle op-count model of exactly this workload (tools/roofline_model.py ->
+    profiles/r3_valu_latency.json, keyed by env, lanes, timed step window and seed) over the live
+    kernel_ms; None when the table has no entry for this run."""
     path = os.path.join(HERE, "profiles", "r3_valu_latency.json")
     try:
         with open(path) as f:
             m = json.load(f)[f"{env_id}:{lanes}:{first}:{last}:{seed}"]
     except (OSError, ValueError, KeyError):
-        return None, None
+        return None
     peak = m["constants"]["valu_peak_flops"]
     ach = m["flops_per_launch"] / (kern_ms * 1e-3)
-    valu = {"achieved": ach / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s", "frac": ach / peak,
+    return {"achieved": ach / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s", "frac": ach / peak,
             "flops_per_launch": m["flops_per_launch"],
             "source": "oracle op counts of this exact workload (tools/roofline_model.py, profiles/r3_valu_latency.json)"}
-    lat = {"floor_ms": m["latency_floor_ms"], "kernel_ms": kern_ms, "frac": m["latency_floor_ms"] / kern_ms,
-           "slowest_lane_dependent_ops": m["slowest_lane_dependent_ops_per_launch"],
-           "model": "mean over the timed launches of the slowest lane's dependent solver ops (velocity updates, position "
-                    "points) x 6 cycles (tools/micro/latbench.hip) / 2.4 GHz; serial LDS phases and TOI bookkeeping not counted"}
-    return valu, lat
+
+
+ISSUE_TABLE = "r4_issue_roofline.json"
+
+
+def load_issue(env_id: int, lanes: int, first: int, last: int, seed: int, kern_ms: float):
+    """roofline.issue: the instruction-issue floor of the lane-steps that set each launch's duration.
+    Each timed launch's slowest lane-step was captured (tools/issue_capture.py) and replayed alone under
+    rocprofv3 (tools/issue_replay.py): SQ_INSTS counts its executed instructions, and a lone wave issues
+    one instruction per 4 cycles of any type (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'), so
+    its floor is 4 x SQ_INSTS cycles at the in-kernel clock (s_memtime / s_memrealtime of the stamps
+    build).  frac = floor / the live kernel_ms.  `lone_wave_ms` is the same lane-step's measured
+    duration alone (kernel trace): the model of the launch (the launch lasts as long as its slowest
+    lane), whose gap to the floor is latency (dependent chains, LDS and memory waits) and whose gap
+    to kernel_ms is co-resident waves.  None when profiles/r4_issue_roofline.json has no entry."""
+    path = os.path.join(HERE, "profiles", ISSUE_TABLE)
+    try:
+        with open(path) as f:
+            m = json.load(f)[f"{env_id}:{lanes}:{first}:{last}:{seed}"]
+    except (OSError, ValueError, KeyError):
+        return None
+    floor_ms = m["issue_floor_us_mean"] * 1e-3
+    lone_ms = m["lone_wave_duration_us_mean"] * 1e-3
+    return {"floor_ms": floor_ms, "kernel_ms": kern_ms, "frac": floor_ms / kern_ms,
+            "lone_wave_ms": lone_ms, "lone_wave_over_kernel": lone_ms / kern_ms,
+            "slowest_lane_instructions": m["slowest_lane_instructions_mean"],
+            "in_kernel_clock_ghz": m["in_kernel_clock_ghz"],
+            "source": f"profiles/{ISSUE_TABLE} (tools/issue_capture.py, issue_replay.py, issue_roofline.py)"}
 
 
 def load_traffic(env_id: int, lanes: int):
@@ -425,7 +448,8 @@ def main():
         algo_bytes = ALGO_BYTES[args.env] * L
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
         traffic = load_traffic(args.env, L)
-        valu, latency = load_valu_latency(args.env, L, args.warmup + 1, args.warmup + K, args.seed, kern_ms)
+        valu = load_valu(args.env, L, args.warmup + 1, args.warmup + K, args.seed, kern_ms)
+        issue = load_issue(args.env, L, args.warmup + 1, args.warmup + K, args.seed, kern_ms)
         line = {
             "metric": "env-steps/sec (whole node) at N envs/GPU",
             "value": value,
@@ -449,10 +473,11 @@ def main():
                          "kernel": "k_step", "kernel_ms": kern_ms,
                          "kernel_ms_timing": timing,
                          "algorithmic_bytes_per_launch": algo_bytes,
-                         "limiter": "latency: the serial Gauss-Seidel chains (velocity sweeps, position passes, TOI) of "
-                                    "the slowest lanes, one wave's VALU issue; not HBM and not MFMA",
+                         "limiter": "instruction issue of the slowest lane's wave (one instruction per 4 cycles, serial "
+                                    "Gauss-Seidel chains: velocity sweeps, position passes, TOI) and its latency stalls; "
+                                    "not HBM and not MFMA",
                          "note": "HBM fraction reported because the north star asks for it (SURVEY.md 8d)",
-                         "valu": valu, "latency": latency},
+                         "valu": valu, "issue": issue},
             "checks": dict(bad, ok=checks_ok),
             "diagnostics": {"counters": ctr,
                             "timed_steps_after_spawn": [args.warmup + 1, args.warmup + K],

@@ -73,13 +73,15 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
         todo = [i for i, s in enumerate(SOURCES) if "mrp_env" not in s or os.path.basename(s) in keep]
         # the reused objects must have been compiled from the current sources and headers: an env
         # unit built before a shared header changed would mix two layouts in one A/B library
+        # (MRP_ALLOW_STALE_UNITS=1 accepts it for an A/B of the listed envs when the edit leaves the
+        # LaneState / EnvOps layout unchanged; mrp_create still checks each unit's compiled dims)
         newest_dep = max(os.path.getmtime(d) for d in DEPS if os.path.exists(d) and d.endswith((".h", ".hip", ".cpp")))
         for i, s in enumerate(SOURCES):
             if i not in todo:
                 objs[i] = os.path.join(base, os.path.basename(s) + ".o")
                 if not os.path.exists(objs[i]):
                     raise FileNotFoundError(f"{objs[i]}: build the default library first")
-                if os.path.getmtime(objs[i]) < newest_dep:
+                if os.path.getmtime(objs[i]) < newest_dep and not os.environ.get("MRP_ALLOW_STALE_UNITS"):
                     raise RuntimeError(f"{objs[i]} is older than a source or header it depends on: rebuild the default "
                                        "library (python -m gym_puzzles_amd.build) before a variant")
 

@@ -8,6 +8,7 @@
 #include <cstddef>
 #include <cstdio>
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -208,6 +209,15 @@ int mrp_create(int env_id, int n_lanes, int device, uint64_t seed, uint64_t lane
         return MRP_E_HIP;
     };
     if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
+    {   // the lanes beyond the first resident set of k_step waves start late (EnvParams::late_prio);
+        // MRP_LATE_PRIO=k (A/B) raises their issue priority to k
+        int cus = 0;
+        if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
+            return fail("hipDeviceGetAttribute", e);
+        ctx->params.late_from = cus * 4 * env_ops(env_id)->step_waves_per_eu;
+        const char* lp = std::getenv("MRP_LATE_PRIO");
+        ctx->params.late_prio = lp ? std::max(0, std::min(3, std::atoi(lp))) : 0;
+    }
     EnvTables all[N_ENVS];
     for (int i = 0; i < N_ENVS; ++i) build_tables(i, all[i]);
     for (int i = 0; i < N_ENVS; ++i)   // every unit keeps its own __constant__ copy
@@ -221,8 +231,15 @@ int mrp_create(int env_id, int n_lanes, int device, uint64_t seed, uint64_t lane
         {(void**)&ctx->d_flags, nl * (ctx->n_agents + 1) * sizeof(int32_t)},
         {(void**)&ctx->d_ctr, CTR_N * sizeof(int64_t)},
     };
-    for (auto& a : allocs)
-        if ((e = hipMalloc(a.p, a.bytes)) != hipSuccess) return fail("hipMalloc", e);
+    // MRP_STATE_ALLOC=contiguous (diagnostic A/B): the lane state as one physically contiguous
+    // allocation (large page fragments, so the GPU TLB covers it with few entries)
+    const char* pol = std::getenv("MRP_STATE_ALLOC");
+    const bool contiguous = pol && std::strcmp(pol, "contiguous") == 0;
+    for (auto& a : allocs) {
+        if (contiguous && a.p == (void**)&ctx->d_state) e = hipExtMallocWithFlags(a.p, a.bytes, hipDeviceMallocContiguous);
+        else e = hipMalloc(a.p, a.bytes);
+        if (e != hipSuccess) return fail("hipMalloc", e);
+    }
     {   // the host API's pinned I/O buffer, carved 16-B aligned: doubles first, then floats, then bytes
         auto up = [](size_t b) { return (b + 15) & ~(size_t)15; };
         const size_t sz_draws = up(nl * ctx->n_draws * sizeof(double)), sz_r64 = up(nl * sizeof(double));
@@ -596,10 +613,10 @@ int mrp_debug_stamps_ext(int device, uint64_t* pmax16, uint64_t* stepmax256, uin
     return rc;
 }
 
-// Diagnostic builds only: the last step's per-lane trace (n_lanes x 24 words, n_lanes <= 16384).
+// Diagnostic builds only: the last step's per-lane trace (n_lanes x 32 words, n_lanes <= 16384).
 int mrp_debug_trace(int device, uint32_t* out, int n_lanes) {
     if (!out || n_lanes <= 0 || n_lanes > 16384 || hipSetDevice(device) != hipSuccess) return MRP_E_ARG;
-    std::vector<uint32_t> tmp((size_t)n_lanes * 24);
+    std::vector<uint32_t> tmp((size_t)n_lanes * 32);
     std::memset(out, 0, tmp.size() * 4);
     int have = 0;
     for (int i = 0; i < N_ENVS; ++i) {   // only the unit that stepped has a non-zero trace

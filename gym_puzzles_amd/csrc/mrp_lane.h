@@ -219,13 +219,25 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t*
     long long toi0 = 0, pos0 = 0;
 #endif
     StateIO<ENV>::load(sh.S, sh.hw_io, state, lane, tid);
+#ifdef MRP_STAMPS
+    if (tid == 0) sh.trace[24] = (uint32_t)(__builtin_amdgcn_s_memtime() - sh.stamp_t0);
+#endif
     load_tables<ENV>(sh.lt, tid);
+#ifdef MRP_STAMPS
+    if (tid == 0) sh.trace[25] = (uint32_t)(__builtin_amdgcn_s_memtime() - sh.stamp_t0);
+#endif
     __syncthreads();
 #ifdef MRP_STAMPS
     toi0 = sh.S.toiEvents; pos0 = sh.S.posIters;
+    if (tid == 0) sh.trace[26] = (uint32_t)(__builtin_amdgcn_s_memtime() - sh.stamp_t0);
 #endif
     MRP_STAMP(0);
     Env<ENV> e(sh, g_table, P, tid);
+    if (P.late_prio > 0 && (int)blockIdx.x >= P.late_from) {   // a late-dispatched lane (EnvParams::late_prio)
+        e.prio_floor = P.late_prio;
+        e.set_prio(P.late_prio);
+        MRP_TRACE(27, (uint32_t)P.late_prio);
+    }
     if (costmax) {   // priority from the lane's previous-step cost relative to the slowest lane's
         const uint64_t c = cost[lane], m = *costmax;
         e.prio_floor = __builtin_amdgcn_readfirstlane(4 * c > 3 * m ? 3 : (2 * c > m ? 2 : (4 * c > m ? 1 : 0)));
@@ -417,7 +429,7 @@ struct Launch {
         using LS = LaneState<ENV>;
         return EnvOps{lane_words<ENV>(), (int)(offsetof(LS, toiEvents) / 4),
                       {D::OBS, D::ACT, D::NDRAW, D::NA, D::NB, D::NF},
-                      StateIO<ENV>::P, LS::C, LS::NCA, StateIO<ENV>::HWW, upload_tables, init, reset, step,
+                      StateIO<ENV>::P, LS::C, LS::NCA, StateIO<ENV>::HWW, MRP_STEP_WAVES_PER_EU, upload_tables, init, reset, step,
                       bodies, faults, counters, render, goals, debug_read, debug_progress};
     }
 };

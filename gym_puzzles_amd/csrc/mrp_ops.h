@@ -62,6 +62,7 @@ struct EnvOps {
     // contact-slot layout of LaneState (mrp_set_state repairs an understated high-water mark cHW):
     // word offset of cnext (the first of `cslot_arrays` contiguous arrays of `cslot_n` words) and of cHW
     int cslot_word, cslot_n, cslot_arrays, chw_word;
+    int step_waves_per_eu;     // k_step's launch bound: resident waves per SIMD (mrp_create: resident lanes)
     hipError_t (*upload_tables)(const EnvTables* all);   // all N_ENVS tables -> this unit's __constant__ copy
     void (*init)(hipStream_t, uint32_t* state, int nl);
     void (*reset)(hipStream_t, uint32_t* state, int nl, const uint8_t* mask, const double* draws, const float* actions,

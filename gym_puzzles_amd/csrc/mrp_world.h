@@ -46,6 +46,15 @@ constexpr int NULLN = -1;
 #endif
 // MRP_SOLVE_NOINLINE_MAIN (A/B): only the main island solve's lanes-path loops out of line (the TOI
 // sub-step solves keep them inlined)
+// The two-body register paths of 3-4 contact islands (sweep_xw / pos_xw) hold three or four contacts'
+// constants in VGPRs; inlined into k_step they pushed its VGPR spills from 9 to 85.  As functions of
+// their own they get the register file to themselves (k_step saves its live registers around the one
+// call per island solve, not per sweep).  MRP_XW_INLINE (A/B) inlines them.
+#ifdef MRP_XW_INLINE
+#define MRP_XW_FN __device__ __forceinline__
+#else
+#define MRP_XW_FN __device__ __attribute__((noinline))
+#endif
 #ifdef MRP_SOLVE_NOINLINE_MAIN
 #define MRP_MAIN_FN __device__ __attribute__((noinline))
 #else
@@ -64,9 +73,10 @@ static __device__ unsigned long long g_stamps[16];     // per-phase sums over la
 static __device__ unsigned long long g_pmax[16];       // per-phase max over lane-steps
 static __device__ unsigned long long g_stepmax[256];   // per step (stepCounter mod 256): slowest lane's total
 static __device__ unsigned long long g_rt[2];          // sums of lane totals: s_memtime ticks, s_memrealtime ticks
-constexpr int MRP_TRACE_W = 24;
+constexpr int MRP_TRACE_W = 32;
 static __device__ uint32_t g_trace[16384][MRP_TRACE_W];   // last step per lane: phases 0-10, total, nc, toi, pos, vel-units,
-                                                       // velocity / position / island-set-up cycles, largest island
+                                                       // velocity / position / island-set-up cycles, largest island,
+                                                       // 24-26 load sub-phases (state, tables, barrier), 27 priority floor
 #define MRP_NOW() __builtin_amdgcn_s_memtime()
 #define MRP_SUB(k, t0) do { if (tid == 0) sh.trace[k] += (uint32_t)(__builtin_amdgcn_s_memtime() - (t0)); } while (0)
 #define MRP_TRACE(k, v) do { if (tid == 0) sh.trace[k] += (v); } while (0)
@@ -277,7 +287,7 @@ template <int ENV> struct Shared {
     double draws[D::NDRAW];
     unsigned long long stamp_t, stamp_t0, stamp_rt0;
 #ifdef MRP_STAMPS
-    uint32_t trace[24];
+    uint32_t trace[32];
 #endif
 };
 
@@ -1226,9 +1236,14 @@ template <int ENV> struct World {
     template <int PCOUNT, class Pick>
     __device__ __forceinline__ static void vel_update_t(const CC& c, Pick pick, P2& ni, P2& ti,
                                                             P2& vA, float& wA, P2& vB, float& wB) {
+        vel_update_m<PCOUNT>(c, c.mA, c.iA, c.mB, c.iB, pick, ni, ti, vA, wA, vB, wB);
+    }
+    // the same with the two bodies' inverse masses / inertias passed in (equal to c.mA .. c.iB: the
+    // solver copies them from the bodies), so a path that holds them per body need not per contact
+    template <int PCOUNT, class Pick>
+    __device__ __forceinline__ static void vel_update_m(const CC& c, const P2 mA, const float iA, const P2 mB, const float iB,
+                                                            Pick pick, P2& ni, P2& ti, P2& vA, float& wA, P2& vB, float& wB) {
         constexpr int pcount = PCOUNT;
-        const P2 mA = c.mA, mB = c.mB;
-        const float iA = c.iA, iB = c.iB;
         // tangent = b2Cross(normal, 1.0f) = (1*n.y, -1*n.x) = (n.y, -n.x) exactly: a half swap and a
         // negation, which fold into the packed instructions' op_sel / neg modifiers
         const P2 normal = c.normal, tangent = p2(normal.y, -normal.x);
@@ -1458,6 +1473,127 @@ template <int ENV> struct World {
                        : solver_velocity_two_p<1, 1>(is, vcs, iters, early_exit);
     }
 
+    // ---------------------------------------------------------------- two-body register paths, 3-4 contacts
+    // The slowest v0 lanes solve islands of 3 or 4 contacts on at most two moving bodies: X, the block,
+    // is A of every contact, against an agent Y (both boxes of the T touch it) and one or two walls
+    // (round 4 capture of the launches' slowest lane-steps, profiles/r4_issue_roofline.json).  On such a
+    // shape every contact is (X, Y) or (X, W) with W static, and MASK (bit i: contact i is (X, W)) is a
+    // template parameter, so every body access is a register and no velocity goes through readlane /
+    // writelane (the lanes path pays 12 readlanes, 6 writelanes and their wait states per update).
+    // A static body's velocity is +0 before and after each update (invMass = invI = 0, so v - 0 * P = +0
+    // and w - 0 * x = +0 for a finite impulse; a non-finite one marks the lane non-finite), so W is a
+    // zero per update and is not written back; X and Y take their inverse masses from the contacts
+    // (the same bits the solver copied into every contact of the body).  Point counts stay runtime
+    // (one wave-uniform branch per update).  Same float operations in the same order as
+    // solver_velocity, same exact early exit as the other register paths.
+#ifdef MRP_XW_PATHS
+    static constexpr bool XW_PATHS = ENV == 0;
+#else
+    // measured (round 4, profiles/r4_ab_xw.txt): +0.5 % in the driver window, -4 % at steps 21-220 and
+    // -6 % over a whole episode (the call and its register saves per island solve); off by default
+    static constexpr bool XW_PATHS = false;
+#endif
+    __device__ __forceinline__ static void xw_update(CC& c, bool wall, bool two, const P2 mX, const float iX, const P2 mY,
+                                                     const float iY, P2& vX, float& wX, P2& vY, float& wY) {
+        asm volatile("" : "+v"(c.normal));   // as cc_update: the tangent formed inside the packed instructions
+        P2 ni, ti;
+        auto pick = [](bool x) { return uni(x); };
+        if (wall) {
+            P2 vW = p2(0.0f, 0.0f);
+            float wW = 0.0f;
+            if (two) vel_update_m<2>(c, mX, iX, pbc(0.0f), 0.0f, pick, ni, ti, vX, wX, vW, wW);
+            else vel_update_m<1>(c, mX, iX, pbc(0.0f), 0.0f, pick, ni, ti, vX, wX, vW, wW);
+        } else {
+            if (two) vel_update_m<2>(c, mX, iX, mY, iY, pick, ni, ti, vX, wX, vY, wY);
+            else vel_update_m<1>(c, mX, iX, mY, iY, pick, ni, ti, vX, wX, vY, wY);
+        }
+        c.ni = ni; c.ti = ti;
+    }
+    template <int MASK, int NC> static constexpr int xw_first_y() {
+        for (int i = 0; i < NC; ++i)
+            if (!((MASK >> i) & 1)) return i;
+        return -1;
+    }
+    template <int NC, int MASK>
+    MRP_XW_FN int sweep_xw(Isl& is, VC* vcs, int iters, bool early_exit, int x, int y, int pcm) {
+        constexpr int FY = xw_first_y<MASK, NC>();
+        constexpr int NS = 6 + 4 * NC;
+        CC c[NC];
+#pragma unroll
+        for (int i = 0; i < NC; ++i) c[i] = load_cc(vcs[i]);
+        const P2 mX = c[0].mA;
+        const float iX = c[0].iA;
+        const P2 mY = FY >= 0 ? c[FY >= 0 ? FY : 0].mB : pbc(0.0f);
+        const float iY = FY >= 0 ? c[FY >= 0 ? FY : 0].iB : 0.0f;
+        P2 vX = p2(is.vvx[x], is.vvy[x]), vY = p2(0.0f, 0.0f);
+        float wX = is.vw[x], wY = 0.0f;
+        if (FY >= 0) { vY = p2(is.vvx[y], is.vvy[y]); wY = is.vw[y]; }
+        auto state = [&](float (&v)[NS]) {
+            v[0] = vX.x; v[1] = vX.y; v[2] = wX; v[3] = vY.x; v[4] = vY.y; v[5] = wY;
+#pragma unroll
+            for (int i = 0; i < NC; ++i) { v[6 + 4 * i] = c[i].ni.x; v[7 + 4 * i] = c[i].ni.y; v[8 + 4 * i] = c[i].ti.x; v[9 + 4 * i] = c[i].ti.y; }
+        };
+        float init[NS];
+        state(init);
+        Snap<NS> snap(init, snap_initial(iters));
+        int sweeps = 0;
+        for (int it = 0; it < iters; ++it) {
+            ++sweeps;
+#pragma unroll
+            for (int i = 0; i < NC; ++i) xw_update(c[i], (MASK >> i) & 1, (pcm >> i) & 1, mX, iX, mY, iY, vX, wX, vY, wY);
+            if (early_exit && ((iters - it - 1) & 1) == 0) {
+                float cur[NS];
+                state(cur);
+                if (snap.step(it, iters, cur)) break;
+            }
+        }
+        if (tid == 0) {
+            is.vvx[x] = vX.x; is.vvy[x] = vX.y; is.vw[x] = wX;
+            if (FY >= 0) { is.vvx[y] = vY.x; is.vvy[y] = vY.y; is.vw[y] = wY; }
+#pragma unroll
+            for (int i = 0; i < NC; ++i) store_cc(vcs[i], c[i]);
+        }
+        return sweeps;
+    }
+    // the island's shape for the two-body paths: (NC, MASK) packed as NC * 16 + MASK with X and Y and
+    // the point-count mask, or -1 when a contact is not (X, Y) / (X, static) or NC is not 3 or 4
+    struct XwShape { int key, x, y, pcm; };
+    __device__ __forceinline__ XwShape xw_shape(const Isl& is, const VC* vcs) const {
+        XwShape r{-1, 0, -1, 0};
+        const int nc = __builtin_amdgcn_readfirstlane(is.nc);
+        if (nc != 3 && nc != 4) return r;
+        const int x = __builtin_amdgcn_readfirstlane(vcs[0].iaI);
+        if (!is_dyn(is.bodies[x])) return r;
+        int y = -1, mask = 0, pcm = 0;
+        for (int i = 0; i < nc; ++i) {
+            const int a = __builtin_amdgcn_readfirstlane(vcs[i].iaI), b = __builtin_amdgcn_readfirstlane(vcs[i].ibI);
+            if (a != x) return r;
+            if (is_dyn(__builtin_amdgcn_readfirstlane(is.bodies[b]))) {
+                if (y >= 0 && b != y) return r;
+                y = b;
+            } else {
+                mask |= 1 << i;
+            }
+            if (__builtin_amdgcn_readfirstlane(vcs[i].pointCount) == 2) pcm |= 1 << i;
+        }
+        r.key = nc * 16 + mask; r.x = x; r.y = y; r.pcm = pcm;
+        return r;
+    }
+    // the shapes instantiated (the v0 driver window's 3-4 contact islands, by velocity updates: (3, 4)
+    // 24 %, (3, 7) 14 %, (4, 15) 13 %, (3, 6) 9 %, (4, 12) 8 %; oracle b2o_topo_diag, round 4)
+    __device__ __forceinline__ int solver_velocity_xw(Isl& is, VC* vcs, int iters, bool early_exit = true) {
+        if constexpr (!XW_PATHS) return -1;
+        const XwShape q = xw_shape(is, vcs);
+        switch (q.key) {
+            case 3 * 16 + 4: return sweep_xw<3, 4>(is, vcs, iters, early_exit, q.x, q.y, q.pcm);
+            case 3 * 16 + 6: return sweep_xw<3, 6>(is, vcs, iters, early_exit, q.x, q.y, q.pcm);
+            case 3 * 16 + 7: return sweep_xw<3, 7>(is, vcs, iters, early_exit, q.x, q.y, q.pcm);
+            case 4 * 16 + 12: return sweep_xw<4, 12>(is, vcs, iters, early_exit, q.x, q.y, q.pcm);
+            case 4 * 16 + 15: return sweep_xw<4, 15>(is, vcs, iters, early_exit, q.x, q.y, q.pcm);
+            default: return -1;
+        }
+    }
+
     // ---------------------------------------------------------------- lane-distributed position iterations
     // b2ContactSolver::SolvePositionConstraints (toi = false) or SolveTOIPositionConstraints
     // (toi = true), repeated until the reference's exit test passes or `iters` passes have run,
@@ -1537,6 +1673,13 @@ template <int ENV> struct World {
     template <class GetA, class GetB, class OnSep>
     __device__ __forceinline__ static void pos_update(const PCC& c, int pcount, int type, float baum, GetA getA, GetB getB,
                                                       OnSep onSep, P2& cA, float& aA, P2& cB, float& aB) {
+        pos_update_m(c, c.mA, c.iA, c.mB, c.iB, pcount, type, baum, getA, getB, onSep, cA, aA, cB, aB);
+    }
+    // the same with the bodies' inverse masses / inertias passed in (see vel_update_m)
+    template <class GetA, class GetB, class OnSep>
+    __device__ __forceinline__ static void pos_update_m(const PCC& c, const P2 mA, const float iA, const P2 mB, const float iB,
+                                                        int pcount, int type, float baum, GetA getA, GetB getB,
+                                                        OnSep onSep, P2& cA, float& aA, P2& cB, float& aB) {
         for (int j = 0; j < 2; ++j) {
             if (j == pcount) break;
             const P2 qA = getA(aA), qB = getB(aB);
@@ -1561,13 +1704,13 @@ template <int ENV> struct World {
             onSep(sep);
             const float Cc = fclamp(baum * (sep + LINEAR_SLOP), -MAX_LINEAR_CORRECTION, 0.0f);
             const float rnA = pcross(rA, normal), rnB = pcross(rB, normal);
-            const float K = c.mA.x + c.mB.x + c.iA * rnA * rnA + c.iB * rnB * rnB;
+            const float K = mA.x + mB.x + iA * rnA * rnA + iB * rnB * rnB;
             const float impulse = K > 0.0f ? -Cc / K : 0.0f;
             const P2 Pv = pbc(impulse) * normal;
-            cA = cA - c.mA * Pv;
-            aA -= c.iA * pcross(rA, Pv);
-            cB = cB + c.mB * Pv;
-            aB += c.iB * pcross(rB, Pv);
+            cA = cA - mA * Pv;
+            aA -= iA * pcross(rA, Pv);
+            cB = cB + mB * Pv;
+            aB += iB * pcross(rB, Pv);
         }
     }
     // the register-resident form: identical lanes, one wave-uniform memo
@@ -1628,6 +1771,70 @@ template <int ENV> struct World {
         if (b0 == a1) return pos_sweep<2, false, false, true>(is, vcs, pcs, toi, toiA, toiB, iters, b0, a0, b1);
         if (b0 == b1) return pos_sweep<2, false, false, false>(is, vcs, pcs, toi, toiA, toiB, iters, b0, a0, a1);
         return -1;
+    }
+
+    // position passes of the two-body shapes of solver_velocity_xw (same masks): X and Y in registers,
+    // each (X, W) contact's static body at its fixed centre and angle (+0): a static body's position is
+    // unchanged by a finite impulse (c + 0 * P = c, a + 0 * x = a), so it is not written back.  Same
+    // float operations in the same order as solver_position; one wave-uniform rotation memo.
+    template <int NC, int MASK>
+    MRP_XW_FN int pos_xw(Isl& is, const VC* vcs, const PC* pcs, int iters, int x, int y) {
+        constexpr int FY = xw_first_y<MASK, NC>();
+        PCC c[NC];
+        P2 cW[NC];
+        float aW[NC];
+#pragma unroll
+        for (int i = 0; i < NC; ++i) {
+            c[i] = load_pcc(vcs[i], pcs[i], false, -1, -1);
+            c[i].pcount = __builtin_amdgcn_readfirstlane(c[i].pcount);
+            c[i].type = __builtin_amdgcn_readfirstlane(c[i].type);
+            const int b = vcs[i].ibI;
+            cW[i] = p2(is.pcx[b], is.pcy[b]);
+            aW[i] = is.pa[b];
+        }
+        const P2 mX = c[0].mA;
+        const float iX = c[0].iA;
+        const P2 mY = FY >= 0 ? c[FY >= 0 ? FY : 0].mB : pbc(0.0f);
+        const float iY = FY >= 0 ? c[FY >= 0 ? FY : 0].iB : 0.0f;
+        P2 cX = p2(is.pcx[x], is.pcy[x]), cY = p2(0.0f, 0.0f);
+        float aX = is.pa[x], aY = 0.0f;
+        if (FY >= 0) { cY = p2(is.pcx[y], is.pcy[y]); aY = is.pa[y]; }
+        UniMemo memo;
+        auto get = [&memo](float a) { return memo.get(a); };
+        int it = 0;
+        while (it < iters) {
+            ++it;
+            float minSep = 0.0f;
+            auto onSep = [&minSep](float sep) { minSep = fmin_(minSep, sep); };
+#pragma unroll
+            for (int i = 0; i < NC; ++i) {
+                if ((MASK >> i) & 1) {
+                    P2 cb = cW[i];
+                    float ab = aW[i];
+                    pos_update_m(c[i], mX, iX, pbc(0.0f), 0.0f, c[i].pcount, c[i].type, BAUMGARTE, get, get, onSep, cX, aX, cb, ab);
+                } else {
+                    pos_update_m(c[i], mX, iX, mY, iY, c[i].pcount, c[i].type, BAUMGARTE, get, get, onSep, cX, aX, cY, aY);
+                }
+            }
+            if (uni(minSep >= -3.0f * LINEAR_SLOP)) break;
+        }
+        if (tid == 0) {
+            is.pcx[x] = cX.x; is.pcy[x] = cX.y; is.pa[x] = aX;
+            if (FY >= 0) { is.pcx[y] = cY.x; is.pcy[y] = cY.y; is.pa[y] = aY; }
+        }
+        return it;
+    }
+    __device__ __forceinline__ int solver_position_xw(Isl& is, const VC* vcs, const PC* pcs, int iters) {
+        if constexpr (!XW_PATHS) return -1;
+        const XwShape q = xw_shape(is, vcs);
+        switch (q.key) {
+            case 3 * 16 + 4: return pos_xw<3, 4>(is, vcs, pcs, iters, q.x, q.y);
+            case 3 * 16 + 6: return pos_xw<3, 6>(is, vcs, pcs, iters, q.x, q.y);
+            case 3 * 16 + 7: return pos_xw<3, 7>(is, vcs, pcs, iters, q.x, q.y);
+            case 4 * 16 + 12: return pos_xw<4, 12>(is, vcs, pcs, iters, q.x, q.y);
+            case 4 * 16 + 15: return pos_xw<4, 15>(is, vcs, pcs, iters, q.x, q.y);
+            default: return -1;
+        }
     }
 
     // position passes of islands of NC = 3 or 4 contacts with the schedule (bodies, point counts,
@@ -1770,6 +1977,7 @@ template <int ENV> struct World {
     __device__ __forceinline__ void island_position(Isl& is, VC* vcs, PC* pcs, int nc) {
         if (nc > 0 && nc <= 64) {
             int n = solver_position_small(is, vcs, pcs, false, -1, -1, 60);
+            if (n < 0) n = solver_position_xw(is, vcs, pcs, 60);
             if (n < 0) n = solver_position_lanes<true>(is, vcs, pcs, false, -1, -1, 60);
             if (tid == 0) S.posIters += n;
         } else if (tid == 0) {
@@ -1857,6 +2065,7 @@ template <int ENV> struct World {
             if (nc > 0 && nc <= 64) {
                 set_prio(lvl > step_prio ? lvl : step_prio);
                 int sweeps = nc == 1 ? solver_velocity_one(is, sh.u.sol.vcs, 180) : (nc == 2 ? solver_velocity_two(is, sh.u.sol.vcs, 180) : -1);
+                if (sweeps < 0) sweeps = solver_velocity_xw(is, sh.u.sol.vcs, 180);
                 if (sweeps < 0) sweeps = solver_velocity_lanes<true>(is, sh.u.sol.vcs, 180);
                 MRP_TRACE(15, sweeps * nc);
                 (void)sweeps;

@@ -15,7 +15,7 @@ NAMES = "load act fnc0 coll solve fnc1 toi obs out reset store".split()
 
 
 def trace(L, n):
-    tr = np.zeros((n, 24), np.uint32)
+    tr = np.zeros((n, 32), np.uint32)
     L.mrp_debug_trace(0, tr.ctypes.data_as(ctypes.c_void_p), n)
     return tr
 
