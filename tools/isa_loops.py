@@ -79,7 +79,14 @@ def analyse(lines):
             elif mm:
                 cur.update(loop=mm.group(1), depth=int(mm.group(2)))
             continue
-        if not s or s.startswith((";", ".")) or s.endswith(":"):
+        if s.startswith(";"):
+            # continuation lines of a block label's annotation (nested loop headers print their
+            # "=> This Inner Loop Header: Depth=d" on a comment line below the label)
+            h = HDR.search(s)
+            if h and cur["loop"] is None or (h and cur["n"] == {} and not cur["header"]):
+                cur.update(loop=cur["label"], depth=int(h.group(1)), header=True)
+            continue
+        if not s or s.startswith(".") or s.endswith(":"):
             continue
         op = s.split()[0]
         k = classify(op)

@@ -32,12 +32,12 @@ def main():
         b.step()
     L = _native.load()
     tr = np.zeros((lanes, 32), np.uint32)
-    acc = np.zeros((lanes, 12), np.float64)
+    acc = np.zeros((lanes, 32), np.float64)
     slow_block = np.zeros((lanes + 1023) // 1024, np.int64)
     for _ in range(steps):
         b.step()
         assert L.mrp_debug_trace(0, tr.ctypes.data_as(ctypes.c_void_p), lanes) == 0
-        acc += tr[:, :12]
+        acc += tr
         slow_block[int(np.argmax(tr[:, 11])) // 1024] += 1
     acc /= steps
     res = {"env": env, "lanes": lanes, "blocks": []}
@@ -45,11 +45,13 @@ def main():
         blk = acc[k * 1024:(k + 1) * 1024]
         res["blocks"].append({"lanes": [k * 1024, min(lanes, (k + 1) * 1024) - 1], "slowest_lane_launches": int(slow_block[k]),
                               "mean_total": float(blk[:, 11].mean()),
-                              "mean_phases": {n: float(blk[:, i].mean()) for i, n in enumerate(NAMES)}})
+                              "mean_phases": {n: float(blk[:, i].mean()) for i, n in enumerate(NAMES)},
+                              # load sub-phases, cycles from the wave's start: state loaded, tables loaded, barrier
+                              "load_marks": [float(blk[:, 24].mean()), float(blk[:, 25].mean()), float(blk[:, 26].mean())]})
         p = res["blocks"][-1]["mean_phases"]
         print(f"lanes {k * 1024:5d}-{min(lanes, (k + 1) * 1024) - 1:5d}: slowest in {slow_block[k]:2d}/{steps} launches, "
               f"mean total {blk[:, 11].mean():9.0f}  load {p['load+act']:8.0f}  solve {p['solve(islands)']:8.0f}  "
-              f"TOI {p['TOI']:8.0f}  store {p['store']:8.0f}")
+              f"TOI {p['TOI']:8.0f}  store {p['store']:8.0f}  load marks " + " ".join(f"{v:8.0f}" for v in res["blocks"][-1]["load_marks"]))
     if out:
         with open(out, "w") as f:
             json.dump(res, f, indent=1)
