@@ -353,12 +353,6 @@ template <int ENV> struct Env : World<ENV> {
 
     // reset(): destroy + rebuild from sh.draws, then the reference's step with sh.act
     __device__ __forceinline__ void env_reset_coop() {
-        env_reset_prelude();
-        env_step_coop();
-    }
-    // reset() up to its step: the contact slots back to their initial contents, the bodies destroyed and
-    // rebuilt from sh.draws, the distances (k_step follows it with its own env_step_coop call site)
-    __device__ __forceinline__ void env_reset_prelude() {
         {   // the contact slots used since the last reset back to their initial contents (destroy_bodies
             // rebuilds the free chain), so every slot is initial again (LaneState::cHW)
             using LS = typename W::LS;
@@ -376,6 +370,7 @@ template <int ENV> struct Env : World<ENV> {
             calc_distances();
         }
         __syncthreads();
+        env_step_coop();
     }
 };
 

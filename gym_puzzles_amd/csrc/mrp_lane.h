@@ -255,48 +255,39 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t*
             sh.act[tid] = actions ? actions[row * D::ACT + tid] : (float)(-1.0 + 2.0 * rng_u01(seed, glane, 3, ctr + tid));
         __syncthreads();
         if (tid == 0) sh.S.stepCounter += 1;
-        // ONE call site of the env step for the step itself (pass 0) and for an auto-reset's step (pass
-        // 1): inlined twice, the world step (collide, islands, solver, TOI) doubled k_step's code (1 MB
-        // for v0), which every lane's phases fetch through the instruction cache
-#pragma nounroll
-        for (int pass = 0; pass < 2; ++pass) {
-            e.env_step_coop();
-            if (pass == 1) {   // the auto-reset's step (reset(): multi_robot_puzzle_00.py:411, _02.py:442)
-                MRP_STAMP(9);
-                break;
-            }
-            // per-lane failure report (SURVEY.md 8b Errors): a NaN / inf in the observation or the
-            // dynamic bodies' state, and a sticky loop-guard fault, set status bits (never a crash)
-            bool nf = false;
-            for (int k = tid; k < D::OBS; k += BLOCK) nf |= !__builtin_isfinite(sh.obs[k]);
-            if (tid < LaneState<ENV>::ND) {
-                const int b = tid;
-                nf |= !__builtin_isfinite(sh.S.cx[b]) || !__builtin_isfinite(sh.S.cy[b]) || !__builtin_isfinite(sh.S.a[b]) ||
-                      !__builtin_isfinite(sh.S.vx[b]) || !__builtin_isfinite(sh.S.vy[b]) || !__builtin_isfinite(sh.S.w[b]);
-            }
-            const bool nonfinite = __builtin_amdgcn_ballot_w64(nf) != 0;
-            if (tid == 0) {
-                sh.S.elapsed += 1;
-                int d = sh.done, tr = 0;
-                if (max_steps > 0 && sh.S.elapsed >= max_steps) { tr = !d; d = 1; }   // gym TimeLimit
-                if (nonfinite) sh.S.nonfinite += 1;
-                if (reward) reward[row] = (float)sh.reward;
-                if (reward64) reward64[row] = sh.reward;   // the reference's Python float
-                if (done_out) done_out[row] = (uint8_t)d;
-                if (trunc_out) trunc_out[row] = (uint8_t)tr;
-                if (status_out)
-                    status_out[row] = (uint8_t)(sh.kind | (nonfinite ? MRP_STATUS_NONFINITE_BIT : 0) |
-                                                (sh.S.fault ? MRP_STATUS_FAULT_BIT : 0));
-                s_fin = d;
-            }
-            __syncthreads();
-            if (term_obs)
-                for (int k = tid; k < D::OBS; k += BLOCK) term_obs[row * D::OBS + k] = sh.obs[k];
-            MRP_STAMP(8);
-            if (!(s_fin && auto_reset)) break;
-            // SB3-style auto-reset with device-RNG spawns: rebuild, then pass 1 runs the reset's step
+        e.env_step_coop();
+        // per-lane failure report (SURVEY.md 8b Errors): a NaN / inf in the observation or the
+        // dynamic bodies' state, and a sticky loop-guard fault, set status bits (never a crash)
+        bool nf = false;
+        for (int k = tid; k < D::OBS; k += BLOCK) nf |= !__builtin_isfinite(sh.obs[k]);
+        if (tid < LaneState<ENV>::ND) {
+            const int b = tid;
+            nf |= !__builtin_isfinite(sh.S.cx[b]) || !__builtin_isfinite(sh.S.cy[b]) || !__builtin_isfinite(sh.S.a[b]) ||
+                  !__builtin_isfinite(sh.S.vx[b]) || !__builtin_isfinite(sh.S.vy[b]) || !__builtin_isfinite(sh.S.w[b]);
+        }
+        const bool nonfinite = __builtin_amdgcn_ballot_w64(nf) != 0;
+        if (tid == 0) {
+            sh.S.elapsed += 1;
+            int d = sh.done, tr = 0;
+            if (max_steps > 0 && sh.S.elapsed >= max_steps) { tr = !d; d = 1; }   // gym TimeLimit
+            if (nonfinite) sh.S.nonfinite += 1;
+            if (reward) reward[row] = (float)sh.reward;
+            if (reward64) reward64[row] = sh.reward;   // the reference's Python float
+            if (done_out) done_out[row] = (uint8_t)d;
+            if (trunc_out) trunc_out[row] = (uint8_t)tr;
+            if (status_out)
+                status_out[row] = (uint8_t)(sh.kind | (nonfinite ? MRP_STATUS_NONFINITE_BIT : 0) |
+                                            (sh.S.fault ? MRP_STATUS_FAULT_BIT : 0));
+            s_fin = d;
+        }
+        __syncthreads();
+        if (term_obs)
+            for (int k = tid; k < D::OBS; k += BLOCK) term_obs[row * D::OBS + k] = sh.obs[k];
+        MRP_STAMP(8);
+        if (s_fin && auto_reset) {   // SB3-style auto-reset with device-RNG spawns
             stage_reset_inputs<ENV>(sh, nullptr, nullptr, lane, tid, seed, glane);
-            e.env_reset_prelude();
+            e.env_reset_coop();
+            MRP_STAMP(9);
         }
         for (int k = tid; k < D::OBS; k += BLOCK) obs[row * D::OBS + k] = sh.obs[k];
         __syncthreads();

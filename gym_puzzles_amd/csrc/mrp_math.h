@@ -257,6 +257,17 @@ MRP_HD Rot rot(float y) {
     return rot_slow(y);
 }
 
+// b2Rot::Set(+-0) = {+-0, 1} exactly (glibc's sinf / cosf return y and 1 below 2^-12): when no
+// active lane's angle is nonzero (a static body's sweep in the TOI iterations, a body whose angle
+// never left zero such as a v0 agent with invI = 0) the wave skips the polynomials; otherwise rot().
+// The position passes keep rot(): their rotation memo already answers +0.
+MRP_HD Rot rot_z(float y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (__builtin_amdgcn_ballot_w64(y != 0.0f) == 0) { Rot q; q.s = y; q.c = 1.0f; return q; }
+#endif
+    return rot(y);
+}
+
 // ---------------------------------------------------------------------------------------
 // Counter-based RNG for on-device resets and synthetic actions (pure integer SplitMix64
 // mixing; identical on host and device, so the CPU oracle can replay device resets).

@@ -320,7 +320,7 @@ template <int ENV> struct World {
     __device__ __forceinline__ V2 center(int b) const { return b < ND ? v2(S.cx[b], S.cy[b]) : v2(L.wall_px[b - ND], L.wall_py[b - ND]); }
     __device__ __forceinline__ V2 lc(int b) const { return v2(L.lcx[b], L.lcy[b]); }
     __device__ __forceinline__ void sync_transform(int b) {   // b2Body::SynchronizeTransform
-        Rot q = rot(S.a[b]);
+        Rot q = rot_z(S.a[b]);
         S.xs[b] = q.s; S.xc[b] = q.c;
         V2 p = vsub(v2(S.cx[b], S.cy[b]), mul_rv(q, lc(b)));
         S.xpx[b] = p.x; S.xpy[b] = p.y;
@@ -504,7 +504,7 @@ template <int ENV> struct World {
     }
     // b2Body::SynchronizeFixtures for a dynamic body, fixtures in fixture-list order (newest first)
     __device__ __forceinline__ void sync_fixtures(int b) {
-        Xf x1; x1.q = rot(S.a0[b]);
+        Xf x1; x1.q = rot_z(S.a0[b]);
         x1.p = vsub(v2(S.c0x[b], S.c0y[b]), mul_rv(x1.q, lc(b)));
         Xf x2 = xf(b);
         for (int k = L.body_nfix[b] - 1; k >= 0; --k) {
@@ -828,7 +828,7 @@ template <int ENV> struct World {
             V2 cB = v2(is.pcx[ib], is.pcy[ib]); float aB = is.pa[ib];
             V2 vB = v2(is.vvx[ib], is.vvy[ib]); float wB = is.vw[ib];
             Xf xA, xB;
-            xA.q = rot(aA); xB.q = rot(aB);
+            xA.q = rot_z(aA); xB.q = rot_z(aB);
             xA.p = vsub(cA, mul_rv(xA.q, v2(pc.lcAx, pc.lcAy)));
             xB.p = vsub(cB, mul_rv(xB.q, v2(pc.lcBx, pc.lcBy)));
             // b2WorldManifold::Initialize
@@ -1013,7 +1013,7 @@ template <int ENV> struct World {
             V2 cB = v2(is.pcx[ib], is.pcy[ib]); float aB = is.pa[ib];
             for (int j = 0; j < pc.pointCount; ++j) {
                 Xf xA, xB;
-                xA.q = rot(aA); xB.q = rot(aB);
+                xA.q = rot_z(aA); xB.q = rot_z(aB);
                 xA.p = vsub(cA, mul_rv(xA.q, v2(pc.lcAx, pc.lcAy)));
                 xB.p = vsub(cB, mul_rv(xB.q, v2(pc.lcBx, pc.lcBy)));
                 V2 normal, point; float sep;
@@ -2104,7 +2104,7 @@ template <int ENV> struct World {
         Xf x;
         x.p = vadd(vmul(1.0f - beta, v2(s.c0x, s.c0y)), vmul(beta, v2(s.cx, s.cy)));
         float angle = (1.0f - beta) * s.a0 + beta * s.a;
-        x.q = rot(angle);
+        x.q = rot_z(angle);
         x.p = vsub(x.p, mul_rv(x.q, v2(s.lcx, s.lcy)));
         return x;
     }
