@@ -217,7 +217,21 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t*
     if (tid == 0) { sh.stamp_t = sh.stamp_t0 = __builtin_amdgcn_s_memtime(); sh.stamp_rt0 = __builtin_amdgcn_s_memrealtime(); }
     if (tid < MRP_TRACE_W) sh.trace[tid] = 0;
     long long toi0 = 0, pos0 = 0;
+    {   // entry probes: 1 KB of straight-line code (instruction fetch), then one load of the lane's
+        // state word cHW (the state load's first access)
+        const unsigned long long p0 = __builtin_amdgcn_s_memtime();
+        asm volatile(".rept 256\n\ts_nop 0\n.endr" ::: "memory");
+        const unsigned long long p1 = __builtin_amdgcn_s_memtime();
+        const uint32_t v = *(volatile const uint32_t*)(state + (size_t)lane * lane_words<ENV>() + StateIO<ENV>::HWW);
+        asm volatile("" :: "v"(v));
+        const unsigned long long p2 = __builtin_amdgcn_s_memtime();
+        if (tid == 0) { sh.trace[20] = (uint32_t)(p1 - p0); sh.trace[21] = (uint32_t)(p2 - p1); }
+    }
 #endif
+    // a late-dispatched lane (EnvParams::late_prio) takes its priority before its state load: at
+    // priority 0 its loads issue behind the resident waves' raised-priority solves
+    const bool late = P.late_prio > 0 && (int)blockIdx.x >= P.late_from;
+    if (late) World<ENV>::set_prio(P.late_prio);
     StateIO<ENV>::load(sh.S, sh.hw_io, state, lane, tid);
 #ifdef MRP_STAMPS
     if (tid == 0) sh.trace[24] = (uint32_t)(__builtin_amdgcn_s_memtime() - sh.stamp_t0);
@@ -233,9 +247,8 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t*
 #endif
     MRP_STAMP(0);
     Env<ENV> e(sh, g_table, P, tid);
-    if (P.late_prio > 0 && (int)blockIdx.x >= P.late_from) {   // a late-dispatched lane (EnvParams::late_prio)
+    if (late) {
         e.prio_floor = P.late_prio;
-        e.set_prio(P.late_prio);
         MRP_TRACE(27, (uint32_t)P.late_prio);
     }
     if (costmax) {   // priority from the lane's previous-step cost relative to the slowest lane's
@@ -292,7 +305,16 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t*
         for (int k = tid; k < D::OBS; k += BLOCK) obs[row * D::OBS + k] = sh.obs[k];
         __syncthreads();
     }
+#ifdef MRP_STAMPS
+    // store sub-stamps (words 22 / 23 replace the island-body diagnostics here): outputs + barrier,
+    // then the LaneState write-back
+    unsigned long long st0 = 0;
+    if (tid == 0) { st0 = __builtin_amdgcn_s_memtime(); sh.trace[22] = (uint32_t)(st0 - sh.stamp_t); }
+#endif
     StateIO<ENV>::store(sh.S, sh.hw_io, state, lane, tid);
+#ifdef MRP_STAMPS
+    if (tid == 0) sh.trace[23] = (uint32_t)(__builtin_amdgcn_s_memtime() - st0);
+#endif
     if (cost && tid == 0) cost[lane] = (uint32_t)min(__builtin_amdgcn_s_memtime() - t_start, 0xffffffffull);
     MRP_STAMP(10);
 #ifdef MRP_STAMPS
@@ -305,6 +327,12 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t*
         sh.trace[11] = (uint32_t)tot;
         sh.trace[13] = (uint32_t)(sh.S.toiEvents - toi0);
         sh.trace[14] = (uint32_t)(sh.S.posIters - pos0);
+        // where and when the lane ran: s_memrealtime (100 MHz, chip-wide) at entry and at the end,
+        // HW_ID (wave / SIMD / CU / SE) and XCC_ID, so a launch's last lane can be named
+        sh.trace[28] = (uint32_t)sh.stamp_rt0;
+        sh.trace[29] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        sh.trace[30] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        sh.trace[31] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);
     }
     __syncthreads();
     if (tid < MRP_TRACE_W && lane < 16384) g_trace[lane][tid] = sh.trace[tid];

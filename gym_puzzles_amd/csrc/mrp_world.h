@@ -1106,15 +1106,15 @@ template <int ENV> struct World {
                 bvx = wrl(bvx, rdl(vA.x, i), ia[i]); bvy = wrl(bvy, rdl(vA.y, i), ia[i]); bw = wrl(bw, rdl(wA, i), ia[i]);
                 bvx = wrl(bvx, rdl(vB.x, i), ib[i]); bvy = wrl(bvy, rdl(vB.y, i), ib[i]); bw = wrl(bw, rdl(wB, i), ib[i]);
             }
-            const int left = iters - (it + 1);
-            if (early_exit && (left & 3) == 0 && have) {
+            const int left = iters - (it + 1), m = exit_mask(it + 1);
+            if (early_exit && (left & m) == 0 && have) {
                 const uint32_t d = (__float_as_uint(my.ni.x) ^ __float_as_uint(sni.x)) | (__float_as_uint(my.ni.y) ^ __float_as_uint(sni.y)) |
                                    (__float_as_uint(my.ti.x) ^ __float_as_uint(sti.x)) | (__float_as_uint(my.ti.y) ^ __float_as_uint(sti.y)) |
                                    (__float_as_uint(bvx) ^ __float_as_uint(sbx)) | (__float_as_uint(bvy) ^ __float_as_uint(sby)) |
                                    (__float_as_uint(bw) ^ __float_as_uint(sbw));
                 if (__builtin_amdgcn_ballot_w64(d != 0u) == 0) break;
             }
-            if (early_exit && (left & 3) == 2) {
+            if (early_exit && (left & m) == 2) {
                 sni = my.ni; sti = my.ti; sbx = bvx; sby = bvy; sbw = bw;
                 have = true;
             }
@@ -1167,15 +1167,15 @@ template <int ENV> struct World {
                 bvx = wrl(bvx, rdl(vA.x, i), ia); bvy = wrl(bvy, rdl(vA.y, i), ia); bw = wrl(bw, rdl(wA, i), ia);
                 bvx = wrl(bvx, rdl(vB.x, i), ib); bvy = wrl(bvy, rdl(vB.y, i), ib); bw = wrl(bw, rdl(wB, i), ib);
             }
-            const int left = iters - (it + 1);   // snapshot at left = 2 mod 4, compare at left = 0 mod 4 (see Snap)
-            if (early_exit && (left & 3) == 0 && have) {
+            const int left = iters - (it + 1), m = exit_mask(it + 1);   // snapshot at left = 2, compare at left = 0 (mod m + 1; see exit_mask)
+            if (early_exit && (left & m) == 0 && have) {
                 const uint32_t d = (__float_as_uint(my.ni.x) ^ __float_as_uint(sni.x)) | (__float_as_uint(my.ni.y) ^ __float_as_uint(sni.y)) |
                                    (__float_as_uint(my.ti.x) ^ __float_as_uint(sti.x)) | (__float_as_uint(my.ti.y) ^ __float_as_uint(sti.y)) |
                                    (__float_as_uint(bvx) ^ __float_as_uint(sbx)) | (__float_as_uint(bvy) ^ __float_as_uint(sby)) |
                                    (__float_as_uint(bw) ^ __float_as_uint(sbw));
                 if (__builtin_amdgcn_ballot_w64(d != 0u) == 0) break;
             }
-            if (early_exit && (left & 3) == 2) {
+            if (early_exit && (left & m) == 2) {
                 sni = my.ni; sti = my.ti; sbx = bvx; sby = bvy; sbw = bw;
                 have = true;
             }
@@ -1359,12 +1359,28 @@ template <int ENV> struct World {
         }
         // one early-exit point after sweep `it + 1` of `iters`
         __device__ __forceinline__ bool step(int it, int iters, const float (&cur)[NS]) {
-            const int left = iters - (it + 1);
-            if ((left & 3) == 0) return same(cur);
-            if ((left & 3) == 2) take(cur);
+            const int left = iters - (it + 1), m = exit_mask(it + 1);
+            if ((left & m) == 0) return same(cur);
+            if ((left & m) == 2) take(cur);
             return false;
         }
     };
+    // The early-exit schedule: after sweep k (left = iters - k) the state is compared with the
+    // snapshot taken two sweeps earlier when left = 0 mod M, and a snapshot is taken when
+    // left = 2 mod M, with M = 4 for the first MRP_EXIT_DENSE sweeps and M = MRP_EXIT_SPARSE after
+    // (both powers of two, so a compare point of either phase has its snapshot exactly two sweeps
+    // before it: left + 2 = 2 mod 4 and mod M).  Any such schedule exits exactly (the state then
+    // has period 1 or 2 and iters - k is even); most islands that repeat do so within a few
+    // sweeps, and the islands that never repeat (the launch's slowest lanes) pay the snapshot and
+    // compare once per M sweeps instead of once per 4.
+#ifndef MRP_EXIT_DENSE
+#define MRP_EXIT_DENSE 32
+#endif
+#ifndef MRP_EXIT_SPARSE
+#define MRP_EXIT_SPARSE 16
+#endif
+    static_assert(MRP_EXIT_SPARSE >= 4 && (MRP_EXIT_SPARSE & (MRP_EXIT_SPARSE - 1)) == 0, "a power of two >= 4");
+    __device__ __forceinline__ static int exit_mask(int done) { return done > MRP_EXIT_DENSE ? MRP_EXIT_SPARSE - 1 : 3; }
     __device__ __forceinline__ static bool snap_initial(int iters) { return (iters & 3) == 2; }   // sweep 0 is a snapshot point
     // register paths: the contacts' point counts (wave-uniform, fixed for the whole solve) select a
     // compile-time instantiation of the sweep loop
@@ -2044,14 +2060,7 @@ template <int ENV> struct World {
                     island_pre(is, h, dtRatio, sh.u.sol.vcs, sh.u.sol.pcs);
                     MRP_SUB(18, tp);
 #ifdef MRP_STAMPS
-                    if ((uint32_t)is.nc > sh.trace[19]) {   // largest island: its contacts' bodies (A << 8 | B)
-                        sh.trace[19] = (uint32_t)is.nc;
-                        for (int k = 0; k < 4; ++k) {
-                            const int c = k < is.nc ? is.contacts[k] : -1;
-                            sh.trace[20 + k] = c < 0 ? 0xffffffffu
-                                             : ((uint32_t)L.fix_body[S.cfa[c]] << 8) | (uint32_t)L.fix_body[S.cfb[c]];
-                        }
-                    }
+                    if ((uint32_t)is.nc > sh.trace[19]) sh.trace[19] = (uint32_t)is.nc;   // largest island's contacts
 #endif
                 }
             }

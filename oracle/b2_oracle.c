@@ -1404,7 +1404,8 @@ void b2o_topo_diag(int on, long* sig64, long* w64) {
 /* CPU-baseline builds (Makefile targets `fast` and `early`, bench.py cpu_baseline): the velocity
  * sweeps without the work model.  OR_EARLY_EXIT stops at the device's exact early exit
  * (mrp_world.h solver_velocity_*): a snapshot two sweeps before every sweep k with 180 - k = 0
- * (mod 4), and once the state after k equals it the state has period 1 or 2, so the state after
+ * (mod 4 up to sweep 32, mod 16 after), and once the state after k equals it the state has period
+ * 1 or 2, so the state after
  * all `iters` sweeps is the state after k -- the same bits, fewer sweeps.  Without OR_EARLY_EXIT
  * all `iters` sweeps run, as b2ContactSolver::SolveVelocityConstraints is called by b2Island::Solve. */
 static void velocity_sweeps(Solver* s, int iters, int nbodies) {
@@ -1429,12 +1430,13 @@ static void velocity_sweeps(Solver* s, int iters, int nbodies) {
     if (have) SWEEP_STATE(snap);
     for (int it = 0; it < iters; ++it) {
         solver_solve_velocity(s);
-        const int left = iters - (it + 1);
-        if ((left & 3) == 0 && have) {
+        /* the device's schedule (mrp_world.h exit_mask): every 4 sweeps up to sweep 32, then every 16 */
+        const int left = iters - (it + 1), m = it + 1 > 32 ? 15 : 3;
+        if ((left & m) == 0 && have) {
             SWEEP_STATE(cur);
             if (memcmp(cur, snap, sizeof(float) * (size_t)ns) == 0) break;
         }
-        if ((left & 3) == 2) { SWEEP_STATE(snap); have = 1; }
+        if ((left & m) == 2) { SWEEP_STATE(snap); have = 1; }
     }
 #undef SWEEP_STATE
     if (snap != snap_st) free(snap);
