@@ -230,7 +230,7 @@ def main():
     ap.add_argument("--seed", type=int, default=17)
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the per-step gather to rank 0")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--schedule", type=int, default=0, help="mrp_set_schedule mode: 1 costliest-first dispatch, 2 cost priority, 3 both")
+    ap.add_argument("--schedule", type=int, default=-1, help="mrp_set_schedule mode: 0 lane order, 1 costliest-first dispatch, 2 cost priority, 3 both; default: the library's per-env choice (mrp_create)")
     ap.add_argument("--time-every", type=int, default=0,
                     help="0 (default): one HIP event pair around all K timed launches on the kernel's stream, kernel_ms = "
                          "that time / K; N >= 1: also bracket every N-th launch (per-launch spread; each marker pair "
@@ -278,7 +278,8 @@ def main():
     torch.cuda.set_stream(stream)
     b.set_stream(stream.cuda_stream)
     b.set_auto_reset(True)
-    b.set_schedule(args.schedule)
+    if args.schedule >= 0:
+        b.set_schedule(args.schedule)
     O = b.obs_dim
     obs = torch.zeros((L, O), dtype=torch.float32, device=dev)
     rew = torch.zeros(L, dtype=torch.float32, device=dev)
@@ -466,7 +467,9 @@ def main():
             "config": {"workload": f"{ENV_NAMES[args.env]}, {L} lanes/GPU, random actions, auto-reset",
                        "lanes_per_gpu": L, "global_lanes": world * L,
                        "parallelism": f"lane-sharded x{world}" + ("" if world == 1 or args.no_gather else " + gather to rank 0/step"),
-                       "vecnormalize": bool(args.vecnormalize)},
+                       "vecnormalize": bool(args.vecnormalize),
+                       "dispatch": ("lane order" if args.schedule == 0 else f"mrp_set_schedule({args.schedule})") if args.schedule >= 0
+                                   else "library default (costliest-first for Heavy-v0 / v3 beyond the resident waves, else lane order)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,

@@ -125,11 +125,6 @@ struct EnvParams {
     double scaled_epsilon;
     double puzzle_complete;            // v3 puzzle_complete_reward (core.py:155), added as is on completion
     int frameskip;                     // world.Step calls per env step (multi_robot_puzzle_02.py:139,476-478)
-    // issue priority (s_setprio) of the lanes whose workgroups are dispatched after the first resident
-    // set (workgroup index >= late_from): they start while the earlier lanes' waves hold the SIMDs'
-    // issue at raised priority (0 = off; k_step, mrp_create)
-    int late_prio;
-    int late_from;
     int pad;
 };
 

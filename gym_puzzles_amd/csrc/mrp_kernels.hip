@@ -83,7 +83,7 @@ struct mrp_ctx {
     uint32_t* d_state = nullptr;
     EnvParams params{};
     int auto_reset = 0;
-    int schedule = 0;            // dispatch lanes costliest-first (mrp_set_schedule; measured slower, off)
+    int schedule = 0;            // 1: dispatch lanes costliest-first (mrp_set_schedule; default set at mrp_create)
     int* d_order = nullptr;      // [n_lanes] lane stepped by workgroup b
     uint32_t* d_cost = nullptr;  // [n_lanes] last step's cycles per lane
     uint32_t* d_costmax = nullptr;   // max of d_cost (priority mode)
@@ -209,14 +209,16 @@ int mrp_create(int env_id, int n_lanes, int device, uint64_t seed, uint64_t lane
         return MRP_E_HIP;
     };
     if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
-    {   // the lanes beyond the first resident set of k_step waves start late (EnvParams::late_prio);
-        // MRP_LATE_PRIO=k (A/B) raises their issue priority to k
+    {   // lanes beyond the first resident set of k_step waves start as earlier ones finish; where
+        // there are such lanes, Heavy-v0 and v3 dispatch the previous step's costliest lanes first
+        // (round 4 A/B, profiles/r4_ab_paired_sweeps_schedule.txt: Heavy-v0 +4 % in the driver
+        // window and +10 % at steps 21-220, v3 +1-2 %; v0 -0.9 % / +1 %, and -3..-5 % at 1024
+        // lanes, where every lane is resident and only the ordering kernel's cost remains)
         int cus = 0;
         if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
             return fail("hipDeviceGetAttribute", e);
-        ctx->params.late_from = cus * 4 * env_ops(env_id)->step_waves_per_eu;
-        const char* lp = std::getenv("MRP_LATE_PRIO");
-        ctx->params.late_prio = lp ? std::max(0, std::min(3, std::atoi(lp))) : 0;
+        const int resident = cus * 4 * env_ops(env_id)->step_waves_per_eu;
+        if ((env_id == 1 || env_id == 5) && n_lanes > resident) ctx->schedule = 1;
     }
     EnvTables all[N_ENVS];
     for (int i = 0; i < N_ENVS; ++i) build_tables(i, all[i]);

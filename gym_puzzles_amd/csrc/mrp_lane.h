@@ -75,6 +75,51 @@ __device__ __forceinline__ void move_words(word_t* lds, word_t* g, int tid) {
 // contents in HBM and are rebuilt in LDS (LaneState::cHW).  `hw` = the slots to move (load: the
 // stored cHW; store: max(cHW at load, cHW now), so slots a reset in this launch zeroed are
 // written back as well).
+//
+// The load issues every global load of a region before its first wait (split issue / put), so a
+// lane's state arrives in two memory round trips (the contact mark, then the live contact slots)
+// instead of one per loop trip (~25 before), and the contact slots move in 16-B granules
+// (round 4 A/B, profiles/r4_ab_batched_load_schedule.txt: v2 +2.9 %, the other configs +0-0.6 %).
+typedef uint4 __attribute__((__may_alias__)) quad_t;
+// words [A, B) of a lane's state: 16-B granules where aligned, single words at the ragged ends
+template <int A, int B>
+struct Span {
+    static constexpr int QA = (A + 3) / 4, QB = B / 4;
+    static constexpr bool QUADS = QA < QB;
+    static constexpr int NQ = QUADS ? (QB - QA + BLOCK - 1) / BLOCK : 0;
+    static constexpr int H = QUADS ? 4 * QA - A : 0, T = QUADS ? B - 4 * QB : 0;
+    static constexpr int NS = QUADS ? 1 : (B - A + BLOCK - 1) / BLOCK;   // single words per thread
+    quad_t q[NQ > 0 ? NQ : 1];
+    word_t s[NS > 0 ? NS : 1];
+    __device__ __forceinline__ static int single(int tid, int k) {
+        if constexpr (QUADS) return tid < H ? A + tid : 4 * QB + (tid - H);
+        else return A + tid + k * BLOCK;
+    }
+    __device__ __forceinline__ static bool has_single(int tid, int k) {
+        if constexpr (QUADS) return tid < H + T;
+        else return A + tid + k * BLOCK < B;
+    }
+    __device__ __forceinline__ void issue(const word_t* g, int tid) {
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) {
+            const int i = QA + tid + k * BLOCK;
+            if (i < QB) q[k] = reinterpret_cast<const quad_t*>(g)[i];
+        }
+#pragma unroll
+        for (int k = 0; k < NS; ++k)
+            if (has_single(tid, k)) s[k] = g[single(tid, k)];
+    }
+    __device__ __forceinline__ void put(word_t* lds, int tid) const {
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) {
+            const int i = QA + tid + k * BLOCK;
+            if (i < QB) reinterpret_cast<quad_t*>(lds)[i] = q[k];
+        }
+#pragma unroll
+        for (int k = 0; k < NS; ++k)
+            if (has_single(tid, k)) lds[single(tid, k)] = s[k];
+    }
+};
 template <int ENV>
 struct StateIO {
     using LS = LaneState<ENV>;
@@ -82,25 +127,79 @@ struct StateIO {
     static constexpr int P = (int)(offsetof(LS, cnext) / 4), Q = (int)(offsetof(LS, inv_dt0) / 4), NW = lane_words<ENV>();
     static constexpr int HWW = (int)(offsetof(LS, cHW) / 4);
     static_assert(Q - P == LS::NCA * C, "contact arrays cnext .. mid[1] are contiguous");
-    template <bool LOAD>
-    __device__ __forceinline__ static void contacts(word_t* lds, word_t* g, int hw, int tid) {
-        for (int i = tid; i < LS::NCA * C; i += BLOCK) {
-            const int c = i % C;
-            if (c < hw) {
-                if (LOAD) lds[P + i] = g[P + i]; else g[P + i] = lds[P + i];
-            } else if (LOAD) {
-                lds[P + i] = i < C ? (c + 1 < C ? (uint32_t)(c + 1) : (uint32_t)NULLN) : 0u;
-            }
+    // The contact slots' words [P, Q): NCA arrays of C words, slot c of array a at word
+    // P + a * C + c; slots below the mark hw are live.  They move in 16-B granules: a granule
+    // with any live word is moved whole.  Its other words hold their initial contents on both
+    // sides (in HBM by the cHW invariant, in LDS because the load puts them there and the step
+    // takes slots only at the mark), and the load replaces them by those contents word by word.
+    struct Contacts {
+        static constexpr int QA = (P + 3) / 4, QB = Q / 4, NQ = (QB - QA + BLOCK - 1) / BLOCK;
+        static constexpr int H = 4 * QA - P, T = Q - 4 * QB;
+        static_assert(QA < QB && H + T < BLOCK, "contact words span whole granules");
+        quad_t q[NQ];
+        word_t s;
+        __device__ __forceinline__ static bool live(int w, int hw) { return (w - P) % C < hw; }
+        __device__ __forceinline__ static word_t init(int w) {
+            const int i = w - P;   // cnext (array 0) chains the free list 0 -> 1 -> ... -> C-1; the rest are 0
+            return i < C ? (i + 1 < C ? (word_t)(i + 1) : (word_t)NULLN) : 0u;
         }
-    }
+        // granule j's first slot; its words are slots c0 .. c0 + 3, wrapping into the next array's
+        // slots 0, 1, 2 (C >= 4), so it is live iff c0 < hw or it wraps and slot 0 is live
+        __device__ __forceinline__ static int slot0(int j) { return (4 * j - P) % C; }
+        __device__ __forceinline__ static bool quad_live(int c0, int hw) { return (c0 < hw) | ((c0 + 3 >= C) & (hw > 0)); }
+        __device__ __forceinline__ static word_t pick(word_t v, int c, int w, int hw) {
+            return (c >= C ? c - C : c) < hw ? v : init(w);
+        }
+        static_assert(C >= 4, "a granule spans at most two arrays");
+        __device__ __forceinline__ static int single(int tid) { return tid < H ? P + tid : 4 * QB + (tid - H); }
+        __device__ __forceinline__ void issue(const word_t* g, int hw, int tid) {
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) {
+                const int j = QA + tid + k * BLOCK;
+                if ((j < QB) & quad_live(slot0(j), hw)) q[k] = reinterpret_cast<const quad_t*>(g)[j];
+            }
+            if ((tid < H + T) & live(single(tid), hw)) s = g[single(tid)];
+        }
+        __device__ __forceinline__ void put(word_t* lds, int hw, int tid) const {
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) {
+                const int j = QA + tid + k * BLOCK;
+                if (j < QB) {
+                    const int c0 = slot0(j);
+                    quad_t v = q[k];
+                    v.x = pick(v.x, c0, 4 * j, hw);
+                    v.y = pick(v.y, c0 + 1, 4 * j + 1, hw);
+                    v.z = pick(v.z, c0 + 2, 4 * j + 2, hw);
+                    v.w = pick(v.w, c0 + 3, 4 * j + 3, hw);
+                    reinterpret_cast<quad_t*>(lds)[j] = v;
+                }
+            }
+            if (tid < H + T) lds[single(tid)] = live(single(tid), hw) ? s : init(single(tid));
+        }
+        __device__ __forceinline__ static void store(const word_t* lds, word_t* g, int hw, int tid) {
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) {
+                const int j = QA + tid + k * BLOCK;
+                if ((j < QB) & quad_live(slot0(j), hw)) reinterpret_cast<quad_t*>(g)[j] = reinterpret_cast<const quad_t*>(lds)[j];
+            }
+            if ((tid < H + T) & live(single(tid), hw)) g[single(tid)] = lds[single(tid)];
+        }
+    };
     // hw_io <- the loaded cHW (clamped to the pool; kept in LDS, not live in registers across the step)
     __device__ __forceinline__ static void load(LS& S, int& hw_io, const uint32_t* __restrict__ gs, int lane, int tid) {
-        word_t* g = const_cast<uint32_t*>(gs) + (size_t)lane * NW;
+        const word_t* g = gs + (size_t)lane * NW;
         word_t* lds = reinterpret_cast<word_t*>(&S);
-        const int hw = min(max((int)__builtin_amdgcn_readfirstlane(g[HWW]), 0), C);
-        move_words<0, P, true>(lds, g, tid);
-        move_words<Q, NW, true>(lds, g, tid);
-        contacts<true>(lds, g, hw, tid);
+        const word_t mark = g[HWW];
+        Span<0, P> head;
+        Span<Q, NW> tail;
+        head.issue(g, tid);
+        tail.issue(g, tid);
+        const int hw = min(max((int)__builtin_amdgcn_readfirstlane(mark), 0), C);
+        Contacts ct;
+        ct.issue(g, hw, tid);
+        head.put(lds, tid);
+        tail.put(lds, tid);
+        ct.put(lds, hw, tid);
         if (tid == 0) hw_io = hw;
     }
     __device__ __forceinline__ static void store(const LS& S, const int& hw_io, uint32_t* __restrict__ gs, int lane, int tid) {
@@ -109,7 +208,7 @@ struct StateIO {
         const int hw = max(hw_io, min(max(S.cHW, 0), C));
         move_words<0, P, false>(lds, g, tid);
         move_words<Q, NW, false>(lds, g, tid);
-        contacts<false>(lds, g, hw, tid);
+        Contacts::store(lds, g, hw, tid);
     }
 };
 
@@ -228,10 +327,6 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t*
         if (tid == 0) { sh.trace[20] = (uint32_t)(p1 - p0); sh.trace[21] = (uint32_t)(p2 - p1); }
     }
 #endif
-    // a late-dispatched lane (EnvParams::late_prio) takes its priority before its state load: at
-    // priority 0 its loads issue behind the resident waves' raised-priority solves
-    const bool late = P.late_prio > 0 && (int)blockIdx.x >= P.late_from;
-    if (late) World<ENV>::set_prio(P.late_prio);
     StateIO<ENV>::load(sh.S, sh.hw_io, state, lane, tid);
 #ifdef MRP_STAMPS
     if (tid == 0) sh.trace[24] = (uint32_t)(__builtin_amdgcn_s_memtime() - sh.stamp_t0);
@@ -247,10 +342,6 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t*
 #endif
     MRP_STAMP(0);
     Env<ENV> e(sh, g_table, P, tid);
-    if (late) {
-        e.prio_floor = P.late_prio;
-        MRP_TRACE(27, (uint32_t)P.late_prio);
-    }
     if (costmax) {   // priority from the lane's previous-step cost relative to the slowest lane's
         const uint64_t c = cost[lane], m = *costmax;
         e.prio_floor = __builtin_amdgcn_readfirstlane(4 * c > 3 * m ? 3 : (2 * c > m ? 2 : (4 * c > m ? 1 : 0)));
@@ -318,13 +409,13 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t*
     if (cost && tid == 0) cost[lane] = (uint32_t)min(__builtin_amdgcn_s_memtime() - t_start, 0xffffffffull);
     MRP_STAMP(10);
 #ifdef MRP_STAMPS
+    // no global atomics here: the totals are folded from the traces by k_stamp_fold after the
+    // launch (up to round 4 this block issued 25 atomics per lane on the same few words, and
+    // the other lanes' loads and stores queued behind them at the L2)
     if (tid == 0) {
         unsigned long long tot = sh.stamp_t - sh.stamp_t0;
-        for (int k = 0; k < 11; ++k) { atomicAdd(&g_stamps[k], (unsigned long long)sh.trace[k]); atomicMax(&g_pmax[k], (unsigned long long)sh.trace[k]); }
-        atomicAdd(&g_rt[0], tot);
-        atomicAdd(&g_rt[1], __builtin_amdgcn_s_memrealtime() - sh.stamp_rt0);
-        atomicMax(&g_stepmax[(sh.S.stepCounter - 1u) & 255u], tot);
         sh.trace[11] = (uint32_t)tot;
+        sh.trace[27] = (sh.S.stepCounter - 1u) & 255u;
         sh.trace[13] = (uint32_t)(sh.S.toiEvents - toi0);
         sh.trace[14] = (uint32_t)(sh.S.posIters - pos0);
         // where and when the lane ran: s_memrealtime (100 MHz, chip-wide) at entry and at the end,
@@ -338,6 +429,44 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t*
     if (tid < MRP_TRACE_W && lane < 16384) g_trace[lane][tid] = sh.trace[tid];
 #endif
 }
+
+#ifdef MRP_STAMPS
+// diagnostic builds: folds one launch's per-lane traces into the stamp totals read by
+// mrp_debug_stamps / mrp_debug_stamps_ext (phase sums and maxima, lane-total sums in s_memtime
+// and s_memrealtime ticks, the slowest lane per step), one workgroup after k_step
+template <int ENV>
+__global__ __launch_bounds__(256) void k_stamp_fold(int nl) {
+    constexpr int R = 25;   // 0-10 phase sums, 11-21 phase maxima, 22/23 total sums, 24 slowest lane of the common step
+    __shared__ unsigned long long red[R][256];
+    const int t = threadIdx.x, n = nl < 16384 ? nl : 16384;
+    unsigned long long acc[R] = {};
+    const uint32_t step0 = n > 0 ? (g_trace[0][27] & 255u) : 0u;
+    for (int l = t; l < n; l += 256) {
+        const uint32_t* w = g_trace[l];
+        for (int k = 0; k < 11; ++k) { acc[k] += w[k]; acc[11 + k] = acc[11 + k] > w[k] ? acc[11 + k] : w[k]; }
+        acc[22] += w[11];
+        acc[23] += (uint32_t)(w[29] - w[28]);
+        if ((w[27] & 255u) == step0) acc[24] = acc[24] > w[11] ? acc[24] : w[11];
+        else atomicMax(&g_stepmax[w[27] & 255u], (unsigned long long)w[11]);   // lanes reset on another step
+    }
+    for (int k = 0; k < R; ++k) red[k][t] = acc[k];
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (t < h)
+            for (int k = 0; k < R; ++k) {
+                const unsigned long long a = red[k][t], b = red[k][t + h];
+                red[k][t] = (k >= 11 && k < 22) || k == 24 ? (a > b ? a : b) : a + b;
+            }
+        __syncthreads();
+    }
+    if (t == 0) {
+        for (int k = 0; k < 11; ++k) { atomicAdd(&g_stamps[k], red[k][0]); atomicMax(&g_pmax[k], red[11 + k][0]); }
+        atomicAdd(&g_rt[0], red[22][0]);
+        atomicAdd(&g_rt[1], red[23][0]);
+        atomicMax(&g_stepmax[step0], red[24][0]);
+    }
+}
+#endif
 
 template <int ENV>
 __global__ __launch_bounds__(BLOCK) void k_bodies(const uint32_t* state, int nl, float* out, int32_t* flags) {
@@ -412,6 +541,9 @@ struct Launch {
             hipLaunchKernelGGL((k_step<ENV, false>), dim3(a.nl), dim3(BLOCK), 0, s, a.state, a.nl, a.actions, a.obs, a.reward,
                                a.reward64, a.done, a.trunc, a.status, a.term_obs, a.P, a.seed, a.lane_offset, a.auto_reset,
                                a.max_steps, a.order, a.cost, a.costmax, 1);
+#ifdef MRP_STAMPS
+        hipLaunchKernelGGL(k_stamp_fold<ENV>, dim3(1), dim3(256), 0, s, a.nl);
+#endif
     }
     static void bodies(hipStream_t s, const uint32_t* state, int nl, float* out, int32_t* flags) {
         hipLaunchKernelGGL(k_bodies<ENV>, dim3(nl), dim3(BLOCK), 0, s, state, nl, out, flags);

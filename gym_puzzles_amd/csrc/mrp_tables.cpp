@@ -297,7 +297,6 @@ void default_params(int env_id, EnvParams& p) {
     p.shaped_bounds = 1000.0; p.shaped_blk_bounds = 100.0; p.shaped_puzzle = 10000.0;
     p.puzzle_complete = 100.0;
     p.frameskip = 1;   // the registered ids and the low-dim v0 obs step the world once (multi_robot_puzzle_00.py:161-162)
-    p.late_prio = 0; p.late_from = 0;   // set by mrp_create from the device
     p.pad = 0;
 }
 

@@ -66,8 +66,9 @@ constexpr int NULLN = -1;
 extern "C" __device__ int mrp_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 
 // Diagnostic phase timing (build with -DMRP_STAMPS; never in the shipped build): thread 0 of
-// every lane accumulates s_memtime deltas per phase in LDS and publishes them into g_stamps /
-// g_pmax once, at the end of its step (no global atomics inside the timed phases).
+// every lane accumulates s_memtime deltas per phase in LDS and writes its trace row to g_trace
+// with plain stores at the end of its step; k_stamp_fold (mrp_lane.h) folds the rows into the
+// totals after the launch, so k_step issues no global atomics.
 #ifdef MRP_STAMPS
 static __device__ unsigned long long g_stamps[16];     // per-phase sums over lane-steps
 static __device__ unsigned long long g_pmax[16];       // per-phase max over lane-steps
@@ -76,7 +77,10 @@ static __device__ unsigned long long g_rt[2];          // sums of lane totals: s
 constexpr int MRP_TRACE_W = 32;
 static __device__ uint32_t g_trace[16384][MRP_TRACE_W];   // last step per lane: phases 0-10, total, nc, toi, pos, vel-units,
                                                        // velocity / position / island-set-up cycles, largest island,
-                                                       // 24-26 load sub-phases (state, tables, barrier), 27 priority floor
+                                                       // 20/21 entry probes (1 KB of code, first state load),
+                                                       // 22/23 store sub-phases (outputs, write-back), 24-26 load
+                                                       // sub-phases (state, tables, barrier), 27 step index mod 256,
+                                                       // 28/29 s_memrealtime at entry / end, 30/31 HW_ID / XCC_ID
 #define MRP_NOW() __builtin_amdgcn_s_memtime()
 #define MRP_SUB(k, t0) do { if (tid == 0) sh.trace[k] += (uint32_t)(__builtin_amdgcn_s_memtime() - (t0)); } while (0)
 #define MRP_TRACE(k, v) do { if (tid == 0) sh.trace[k] += (v); } while (0)
@@ -1382,6 +1386,28 @@ template <int ENV> struct World {
     static_assert(MRP_EXIT_SPARSE >= 4 && (MRP_EXIT_SPARSE & (MRP_EXIT_SPARSE - 1)) == 0, "a power of two >= 4");
     __device__ __forceinline__ static int exit_mask(int done) { return done > MRP_EXIT_DENSE ? MRP_EXIT_SPARSE - 1 : 3; }
     __device__ __forceinline__ static bool snap_initial(int iters) { return (iters & 3) == 2; }   // sweep 0 is a snapshot point
+    // The sweep loop of the register paths: `sweep()` runs one Gauss-Seidel sweep, `state(v)` names
+    // the NS values of the sweep state.  Every compare point has iters - k even, so the sweeps run in
+    // pairs and the loop carries no per-sweep parity test or exit bookkeeping (an odd count runs its
+    // first sweep alone); returns the sweeps run.
+    template <int NS, class Sweep, class State>
+    __device__ __forceinline__ static int sweep_pairs(int iters, bool early_exit, Sweep sweep, State state) {
+        int it = 0;
+        if (iters & 1) { sweep(); it = 1; }
+        float cur[NS];
+        state(cur);
+        Snap<NS> snap(cur, ((iters - it) & 3) == 2);
+        while (it < iters) {
+            sweep();
+            sweep();
+            it += 2;
+            if (early_exit) {
+                state(cur);
+                if (snap.step(it - 1, iters, cur)) break;
+            }
+        }
+        return it;
+    }
     // register paths: the contacts' point counts (wave-uniform, fixed for the whole solve) select a
     // compile-time instantiation of the sweep loop
     __device__ __forceinline__ int solver_velocity_one(Isl& is, VC* vcs, int iters, bool early_exit = true) {
@@ -1394,17 +1420,9 @@ template <int ENV> struct World {
         const int ia = vcs[0].iaI, ib = vcs[0].ibI;
         P2 vA = p2(is.vvx[ia], is.vvy[ia]); float wA = is.vw[ia];
         P2 vB = p2(is.vvx[ib], is.vvy[ib]); float wB = is.vw[ib];
-        const float init[10] = {vA.x, vA.y, wA, vB.x, vB.y, wB, c.ni.x, c.ni.y, c.ti.x, c.ti.y};
-        Snap<10> snap(init, snap_initial(iters));
-        int sweeps = 0;
-        for (int it = 0; it < iters; ++it) {
-            ++sweeps;
-            cc_update<P0>(c, vA, wA, vB, wB);
-            if (early_exit && ((iters - it - 1) & 1) == 0) {
-                const float cur[10] = {vA.x, vA.y, wA, vB.x, vB.y, wB, c.ni.x, c.ni.y, c.ti.x, c.ti.y};
-                if (snap.step(it, iters, cur)) break;
-            }
-        }
+        const int sweeps = sweep_pairs<10>(iters, early_exit, [&] { cc_update<P0>(c, vA, wA, vB, wB); }, [&](float (&v)[10]) {
+            v[0] = vA.x; v[1] = vA.y; v[2] = wA; v[3] = vB.x; v[4] = vB.y; v[5] = wB; v[6] = c.ni.x; v[7] = c.ni.y; v[8] = c.ti.x; v[9] = c.ti.y;
+        });
         if (tid == 0) {
             is.vvx[ia] = vA.x; is.vvy[ia] = vA.y; is.vw[ia] = wA;
             is.vvx[ib] = vB.x; is.vvy[ib] = vB.y; is.vw[ib] = wB;
@@ -1420,20 +1438,13 @@ template <int ENV> struct World {
         CC c0 = load_cc(vcs[0]), c1 = load_cc(vcs[1]);
         P2 vX = p2(is.vvx[x], is.vvy[x]), vY = p2(is.vvx[y], is.vvy[y]), vZ = p2(is.vvx[z], is.vvy[z]);
         float wX = is.vw[x], wY = is.vw[y], wZ = is.vw[z];
-        const float init[17] = {vX.x, vX.y, wX, vY.x, vY.y, wY, vZ.x, vZ.y, wZ, c0.ni.x, c0.ni.y, c0.ti.x, c0.ti.y,
-                                c1.ni.x, c1.ni.y, c1.ti.x, c1.ti.y};
-        Snap<17> snap(init, snap_initial(iters));
-        int sweeps = 0;
-        for (int it = 0; it < iters; ++it) {
-            ++sweeps;
+        const int sweeps = sweep_pairs<17>(iters, early_exit, [&] {
             if (XA0) cc_update<P0>(c0, vX, wX, vY, wY); else cc_update<P0>(c0, vY, wY, vX, wX);
             if (XA1) cc_update<P1>(c1, vX, wX, vZ, wZ); else cc_update<P1>(c1, vZ, wZ, vX, wX);
-            if (early_exit && ((iters - it - 1) & 1) == 0) {
-                const float cur[17] = {vX.x, vX.y, wX, vY.x, vY.y, wY, vZ.x, vZ.y, wZ, c0.ni.x, c0.ni.y, c0.ti.x, c0.ti.y,
-                                       c1.ni.x, c1.ni.y, c1.ti.x, c1.ti.y};
-                if (snap.step(it, iters, cur)) break;
-            }
-        }
+        }, [&](float (&v)[17]) {
+            v[0] = vX.x; v[1] = vX.y; v[2] = wX; v[3] = vY.x; v[4] = vY.y; v[5] = wY; v[6] = vZ.x; v[7] = vZ.y; v[8] = wZ;
+            v[9] = c0.ni.x; v[10] = c0.ni.y; v[11] = c0.ti.x; v[12] = c0.ti.y; v[13] = c1.ni.x; v[14] = c1.ni.y; v[15] = c1.ti.x; v[16] = c1.ti.y;
+        });
         if (tid == 0) {   // contact 1 stores last, as the reference's per-contact write-back order leaves it
             is.vvx[x] = vX.x; is.vvy[x] = vX.y; is.vw[x] = wX;
             is.vvx[y] = vY.x; is.vvy[y] = vY.y; is.vw[y] = wY;
@@ -1449,18 +1460,13 @@ template <int ENV> struct World {
         CC c0 = load_cc(vcs[0]), c1 = load_cc(vcs[1]);
         P2 vP = p2(is.vvx[p], is.vvy[p]), vQ = p2(is.vvx[q], is.vvy[q]);
         float wP = is.vw[p], wQ = is.vw[q];
-        const float init[14] = {vP.x, vP.y, wP, vQ.x, vQ.y, wQ, c0.ni.x, c0.ni.y, c0.ti.x, c0.ti.y, c1.ni.x, c1.ni.y, c1.ti.x, c1.ti.y};
-        Snap<14> snap(init, snap_initial(iters));
-        int sweeps = 0;
-        for (int it = 0; it < iters; ++it) {
-            ++sweeps;
+        const int sweeps = sweep_pairs<14>(iters, early_exit, [&] {
             cc_update<P0>(c0, vP, wP, vQ, wQ);
             if (SAME) cc_update<P1>(c1, vP, wP, vQ, wQ); else cc_update<P1>(c1, vQ, wQ, vP, wP);
-            if (early_exit && ((iters - it - 1) & 1) == 0) {
-                const float cur[14] = {vP.x, vP.y, wP, vQ.x, vQ.y, wQ, c0.ni.x, c0.ni.y, c0.ti.x, c0.ti.y, c1.ni.x, c1.ni.y, c1.ti.x, c1.ti.y};
-                if (snap.step(it, iters, cur)) break;
-            }
-        }
+        }, [&](float (&v)[14]) {
+            v[0] = vP.x; v[1] = vP.y; v[2] = wP; v[3] = vQ.x; v[4] = vQ.y; v[5] = wQ;
+            v[6] = c0.ni.x; v[7] = c0.ni.y; v[8] = c0.ti.x; v[9] = c0.ti.y; v[10] = c1.ni.x; v[11] = c1.ni.y; v[12] = c1.ti.x; v[13] = c1.ti.y;
+        });
         if (tid == 0) {
             is.vvx[p] = vP.x; is.vvy[p] = vP.y; is.vw[p] = wP;
             is.vvx[q] = vQ.x; is.vvy[q] = vQ.y; is.vw[q] = wQ;

@@ -1368,7 +1368,8 @@ static int work_velocity_sweeps(Solver* s, int iters, int nbodies) {
     return run >= 0 ? run : iters;
 }
 
-/* diagnostic (b2o_topo_diag): island topologies of 3- and 4-contact islands, weighted by sweeps run:
+/* diagnostic (b2o_topo_diag(1); b2o_topo_diag(2) also records 1- and 2-contact islands): island
+ * topologies of 3- and 4-contact islands, weighted by sweeps run:
  * per contact (A slot, B slot, point count) with body slots numbered by first appearance and static
  * bodies as slot 7; 64 distinct signatures kept */
 static int g_topo_diag = 0;
@@ -1489,7 +1490,7 @@ static void island_solve(Island* is, World* w, TimeStep step) {
         ++passes;
         if (solver_solve_position(&s, 0, -1, -1)) break;
     }
-    if (g_topo_diag && is->contactCount >= 3 && is->contactCount <= 4) topo_record(&s, is, sweeps);
+    if (g_topo_diag && is->contactCount >= (g_topo_diag > 1 ? 1 : 3) && is->contactCount <= 4) topo_record(&s, is, sweeps);
     if (is->contactCount > 0) {
         int dyn[256], lp = 0, pts = 0, n1 = 0, n2 = 0;
         for (int k = 0; k < is->bodyCount && k < 256; ++k) dyn[k] = is->bodies[k]->invMass > 0.0f || is->bodies[k]->invI > 0.0f;

@@ -27,6 +27,8 @@ def main():
     out = sys.argv[5] if len(sys.argv) > 5 else None
     b = Batch(env, lanes, seed=17)
     b.set_auto_reset(True)
+    if "MRP_SCHEDULE" in os.environ:   # 0 lane order, 1 costliest-first dispatch (lane blocks then mix)
+        b.set_schedule(int(os.environ["MRP_SCHEDULE"]))
     b.reset()
     for _ in range(warmup):
         b.step()
