@@ -69,8 +69,8 @@ def one(d, env):
     assert len(pmc) == n, (len(pmc), n)
     reps = len(dur) // n
     dur = np.array(dur[:n * reps]).reshape(n, reps).min(axis=1)   # lone-wave duration, best of the repeats
-    ph = json.load(open(os.path.join(d, "..", f"r4_phase_env{env}.json"))) if os.path.exists(
-        os.path.join(d, "..", f"r4_phase_env{env}.json")) else None
+    cand = [os.path.join(d, f"r4_phase_env{env}.json"), os.path.join(d, "..", f"r4_phase_env{env}.json")]
+    ph = next((json.load(open(c)) for c in cand if os.path.exists(c)), None)
     ghz = ph["s_memtime_ghz"] if ph else 2.2
     inst = {c: np.array([p.get(c, np.nan) for p in pmc]) for c in COUNTERS}
     floor_cyc = 4.0 * inst["SQ_INSTS"]
