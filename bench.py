@@ -464,7 +464,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32 (engine) + f64 (env arithmetic)",
             "data": "synthetic: device-RNG random actions, device-RNG spawns (reference draw ranges)",
-            "config": {"workload": f"{ENV_NAMES[args.env]}, {L} lanes/GPU, random actions, auto-reset",
+            "config": {"workload": f"{ENV_NAMES[args.env]}, {L} lanes/GPU, random actions, auto-reset", "env_id": args.env,
                        "lanes_per_gpu": L, "global_lanes": world * L,
                        "parallelism": f"lane-sharded x{world}" + ("" if world == 1 or args.no_gather else " + gather to rank 0/step"),
                        "vecnormalize": bool(args.vecnormalize),

@@ -29,8 +29,15 @@ DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("mrp_math.h", "mrp_config.h", 
 # and +6.6 % at steps 21-220 (A/B, profiles/r3g_ab_scheduler.txt).  For v0 the same build gives
 # +1.5 % in the driver window but -2.7 % at steps 21-220 (a call per island solve), so v0 keeps the
 # inlined form.  Heavy-v0 (env 1, 5 agents): +1.4 % / +2.0 % (profiles/r3g_ab_scheduler.txt).
-_ILP_LOOPS = ["-DMRP_SOLVE_NOINLINE_LANES", "-mllvm", "-amdgpu-sched-strategy=max-ilp"]
-UNIT_FLAGS = {"mrp_env1.hip": _ILP_LOOPS, "mrp_env4.hip": _ILP_LOOPS}
+# Round 4 (profiles/r4_ab_unit_flags.txt): Heavy-v0 keeps the max-ilp scheduler with the loops
+# inlined (+3.3 % in the driver window, +2.3 % at steps 21-220, PMC traffic 80.7 -> 49.4 MB per
+# launch: no call-site register saves), while the 3-block config loses 5 % that way and keeps its
+# loops out of line; v0 and v3 run the lanes-path sweeps two per loop trip (-DMRP_LANES_PAIRS=1:
+# v0 +1.8 % / +0.7 %, v3 +0.5 %; Heavy-v0 -3 %, 3-block -0.3 %, so those keep one per trip).
+_MAX_ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+_ILP_LOOPS = ["-DMRP_SOLVE_NOINLINE_LANES"] + _MAX_ILP
+_LANES_PAIRS = ["-DMRP_LANES_PAIRS=1"]
+UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS, "mrp_env1.hip": _MAX_ILP, "mrp_env4.hip": _ILP_LOOPS, "mrp_env5.hip": _LANES_PAIRS}
 # -fno-slp-vectorize: the serial solver chains are latency-bound; packing pairs of f32 ops into
 # v_pk_* costs operand-shuffling moves on the dependency chain (measured +2-3 % env-steps/s off)
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",

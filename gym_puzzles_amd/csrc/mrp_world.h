@@ -50,6 +50,11 @@ constexpr int NULLN = -1;
 // constants in VGPRs; inlined into k_step they pushed its VGPR spills from 9 to 85.  As functions of
 // their own they get the register file to themselves (k_step saves its live registers around the one
 // call per island solve, not per sweep).  MRP_XW_INLINE (A/B) inlines them.
+// MRP_LANES_PAIRS=1: the lanes-path sweeps two per loop trip (lanes_sweeps; build.py sets it for the
+// v0 and v3 units, where it measured faster)
+#ifndef MRP_LANES_PAIRS
+#define MRP_LANES_PAIRS 0
+#endif
 #ifdef MRP_XW_INLINE
 #define MRP_XW_FN __device__ __forceinline__
 #else
@@ -1094,12 +1099,7 @@ template <int ENV> struct World {
         int ia[NC], ib[NC], pc[NC];
 #pragma unroll
         for (int i = 0; i < NC; ++i) { ia[i] = rdli(cia, i); ib[i] = rdli(cib, i); pc[i] = rdli(my.pcount, i); }
-        P2 sni = my.ni, sti = my.ti;
-        float sbx = bvx, sby = bvy, sbw = bw;
-        bool have = snap_initial(iters);
-        int sweeps = 0;
-        for (int it = 0; it < iters; ++it) {
-            ++sweeps;
+        auto sweep = [&] {
 #pragma unroll
             for (int i = 0; i < NC; ++i) {
                 P2 vA = p2(rdl(bvx, ia[i]), rdl(bvy, ia[i])); float wA = rdl(bw, ia[i]);
@@ -1110,7 +1110,20 @@ template <int ENV> struct World {
                 bvx = wrl(bvx, rdl(vA.x, i), ia[i]); bvy = wrl(bvy, rdl(vA.y, i), ia[i]); bw = wrl(bw, rdl(wA, i), ia[i]);
                 bvx = wrl(bvx, rdl(vB.x, i), ib[i]); bvy = wrl(bvy, rdl(vB.y, i), ib[i]); bw = wrl(bw, rdl(wB, i), ib[i]);
             }
-            const int left = iters - (it + 1), m = exit_mask(it + 1);
+        };
+        // MRP_LANES_PAIRS: two sweeps per loop trip, as sweep_pairs (an odd count runs its first sweep
+        // alone); the exit bookkeeping then runs once per pair
+        constexpr int STEP = MRP_LANES_PAIRS ? 2 : 1;
+        int sweeps = 0;
+        if (STEP == 2 && (iters & 1)) { sweep(); sweeps = 1; }
+        P2 sni = my.ni, sti = my.ti;
+        float sbx = bvx, sby = bvy, sbw = bw;
+        bool have = ((iters - sweeps) & 3) == 2;   // the start is a snapshot point
+        while (sweeps < iters) {
+            sweep();
+            if (STEP == 2) sweep();
+            sweeps += STEP;
+            const int left = iters - sweeps, m = exit_mask(sweeps);
             if (early_exit && (left & m) == 0 && have) {
                 const uint32_t d = (__float_as_uint(my.ni.x) ^ __float_as_uint(sni.x)) | (__float_as_uint(my.ni.y) ^ __float_as_uint(sni.y)) |
                                    (__float_as_uint(my.ti.x) ^ __float_as_uint(sti.x)) | (__float_as_uint(my.ti.y) ^ __float_as_uint(sti.y)) |
