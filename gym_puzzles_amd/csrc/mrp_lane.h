@@ -78,8 +78,8 @@ __device__ __forceinline__ void move_words(word_t* lds, word_t* g, int tid) {
 //
 // The load issues every global load of a region before its first wait (split issue / put), so a
 // lane's state arrives in two memory round trips (the contact mark, then the live contact slots)
-// instead of one per loop trip (~25 before), and the contact slots move in 16-B granules
-// (round 4 A/B, profiles/r4_ab_batched_load_schedule.txt: v2 +2.9 %, the other configs +0-0.6 %).
+// instead of one per loop trip (~25 before) (round 4 A/B, profiles/r4_ab_batched_load_schedule.txt
+// and r4_ab_contact_words.txt: v2 +2.9 %, the other configs +0-0.6 %).
 typedef uint4 __attribute__((__may_alias__)) quad_t;
 // words [A, B) of a lane's state: 16-B granules where aligned, single words at the ragged ends
 template <int A, int B>
@@ -128,61 +128,38 @@ struct StateIO {
     static constexpr int HWW = (int)(offsetof(LS, cHW) / 4);
     static_assert(Q - P == LS::NCA * C, "contact arrays cnext .. mid[1] are contiguous");
     // The contact slots' words [P, Q): NCA arrays of C words, slot c of array a at word
-    // P + a * C + c; slots below the mark hw are live.  They move in 16-B granules: a granule
-    // with any live word is moved whole.  Its other words hold their initial contents on both
-    // sides (in HBM by the cHW invariant, in LDS because the load puts them there and the step
-    // takes slots only at the mark), and the load replaces them by those contents word by word.
+    // P + a * C + c; only slots below the mark hw are live and move (word by word: moving whole
+    // 16-B granules of the live runs measured the same time and 23 % more PMC traffic for v0).
+    // The load issues every live word's load before the first wait and puts the initial contents
+    // into the other words.
     struct Contacts {
-        static constexpr int QA = (P + 3) / 4, QB = Q / 4, NQ = (QB - QA + BLOCK - 1) / BLOCK;
-        static constexpr int H = 4 * QA - P, T = Q - 4 * QB;
-        static_assert(QA < QB && H + T < BLOCK, "contact words span whole granules");
-        quad_t q[NQ];
-        word_t s;
-        __device__ __forceinline__ static bool live(int w, int hw) { return (w - P) % C < hw; }
-        __device__ __forceinline__ static word_t init(int w) {
-            const int i = w - P;   // cnext (array 0) chains the free list 0 -> 1 -> ... -> C-1; the rest are 0
+        static constexpr int NWC = LS::NCA * C, NK = (NWC + BLOCK - 1) / BLOCK;
+        word_t w[NK];
+        __device__ __forceinline__ static bool live(int i, int hw) { return i % C < hw; }   // i: word of the region
+        __device__ __forceinline__ static word_t init(int i) {
+            // cnext (array 0) chains the free list 0 -> 1 -> ... -> C-1; the other arrays are 0
             return i < C ? (i + 1 < C ? (word_t)(i + 1) : (word_t)NULLN) : 0u;
         }
-        // granule j's first slot; its words are slots c0 .. c0 + 3, wrapping into the next array's
-        // slots 0, 1, 2 (C >= 4), so it is live iff c0 < hw or it wraps and slot 0 is live
-        __device__ __forceinline__ static int slot0(int j) { return (4 * j - P) % C; }
-        __device__ __forceinline__ static bool quad_live(int c0, int hw) { return (c0 < hw) | ((c0 + 3 >= C) & (hw > 0)); }
-        __device__ __forceinline__ static word_t pick(word_t v, int c, int w, int hw) {
-            return (c >= C ? c - C : c) < hw ? v : init(w);
-        }
-        static_assert(C >= 4, "a granule spans at most two arrays");
-        __device__ __forceinline__ static int single(int tid) { return tid < H ? P + tid : 4 * QB + (tid - H); }
         __device__ __forceinline__ void issue(const word_t* g, int hw, int tid) {
 #pragma unroll
-            for (int k = 0; k < NQ; ++k) {
-                const int j = QA + tid + k * BLOCK;
-                if ((j < QB) & quad_live(slot0(j), hw)) q[k] = reinterpret_cast<const quad_t*>(g)[j];
+            for (int k = 0; k < NK; ++k) {
+                const int i = tid + k * BLOCK;
+                if ((i < NWC) & live(i, hw)) w[k] = g[P + i];
             }
-            if ((tid < H + T) & live(single(tid), hw)) s = g[single(tid)];
         }
         __device__ __forceinline__ void put(word_t* lds, int hw, int tid) const {
 #pragma unroll
-            for (int k = 0; k < NQ; ++k) {
-                const int j = QA + tid + k * BLOCK;
-                if (j < QB) {
-                    const int c0 = slot0(j);
-                    quad_t v = q[k];
-                    v.x = pick(v.x, c0, 4 * j, hw);
-                    v.y = pick(v.y, c0 + 1, 4 * j + 1, hw);
-                    v.z = pick(v.z, c0 + 2, 4 * j + 2, hw);
-                    v.w = pick(v.w, c0 + 3, 4 * j + 3, hw);
-                    reinterpret_cast<quad_t*>(lds)[j] = v;
-                }
+            for (int k = 0; k < NK; ++k) {
+                const int i = tid + k * BLOCK;
+                if (i < NWC) lds[P + i] = live(i, hw) ? w[k] : init(i);
             }
-            if (tid < H + T) lds[single(tid)] = live(single(tid), hw) ? s : init(single(tid));
         }
         __device__ __forceinline__ static void store(const word_t* lds, word_t* g, int hw, int tid) {
 #pragma unroll
-            for (int k = 0; k < NQ; ++k) {
-                const int j = QA + tid + k * BLOCK;
-                if ((j < QB) & quad_live(slot0(j), hw)) reinterpret_cast<quad_t*>(g)[j] = reinterpret_cast<const quad_t*>(lds)[j];
+            for (int k = 0; k < NK; ++k) {
+                const int i = tid + k * BLOCK;
+                if ((i < NWC) & live(i, hw)) g[P + i] = lds[P + i];
             }
-            if ((tid < H + T) & live(single(tid), hw)) g[single(tid)] = lds[single(tid)];
         }
     };
     // hw_io <- the loaded cHW (clamped to the pool; kept in LDS, not live in registers across the step)
@@ -316,16 +293,6 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t*
     if (tid == 0) { sh.stamp_t = sh.stamp_t0 = __builtin_amdgcn_s_memtime(); sh.stamp_rt0 = __builtin_amdgcn_s_memrealtime(); }
     if (tid < MRP_TRACE_W) sh.trace[tid] = 0;
     long long toi0 = 0, pos0 = 0;
-    {   // entry probes: 1 KB of straight-line code (instruction fetch), then one load of the lane's
-        // state word cHW (the state load's first access)
-        const unsigned long long p0 = __builtin_amdgcn_s_memtime();
-        asm volatile(".rept 256\n\ts_nop 0\n.endr" ::: "memory");
-        const unsigned long long p1 = __builtin_amdgcn_s_memtime();
-        const uint32_t v = *(volatile const uint32_t*)(state + (size_t)lane * lane_words<ENV>() + StateIO<ENV>::HWW);
-        asm volatile("" :: "v"(v));
-        const unsigned long long p2 = __builtin_amdgcn_s_memtime();
-        if (tid == 0) { sh.trace[20] = (uint32_t)(p1 - p0); sh.trace[21] = (uint32_t)(p2 - p1); }
-    }
 #endif
     StateIO<ENV>::load(sh.S, sh.hw_io, state, lane, tid);
 #ifdef MRP_STAMPS

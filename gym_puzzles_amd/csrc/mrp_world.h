@@ -82,7 +82,7 @@ static __device__ unsigned long long g_rt[2];          // sums of lane totals: s
 constexpr int MRP_TRACE_W = 32;
 static __device__ uint32_t g_trace[16384][MRP_TRACE_W];   // last step per lane: phases 0-10, total, nc, toi, pos, vel-units,
                                                        // velocity / position / island-set-up cycles, largest island,
-                                                       // 20/21 entry probes (1 KB of code, first state load),
+                                                       // 20/21 TOI split (candidate scan + b2TimeOfImpact, events),
                                                        // 22/23 store sub-phases (outputs, write-back), 24-26 load
                                                        // sub-phases (state, tables, barrier), 27 step index mod 256,
                                                        // 28/29 s_memrealtime at entry / end, 30/31 HW_ID / XCC_ID
@@ -2530,6 +2530,7 @@ template <int ENV> struct World {
         for (int pass = 0;; ++pass) {
             MRP_PROG(0x2000u + pass);
             if (pass > (MAX_SUBSTEPS + 1) * C + 2) { if (tid == 0) S.fault = MRP_FAULT_TOI_PASSES; break; }
+            const unsigned long long ts = MRP_NOW();
             if (tid == 0) toi_scan();
             __syncthreads();
             const int tn = sh.tn;
@@ -2541,6 +2542,8 @@ template <int ENV> struct World {
                 sh.u.toi.tout[i] = time_of_impact(pA, pB, sh.u.toi.tsA[i], sh.u.toi.tsB[i]);
             }
             __syncthreads();
+            MRP_SUB(20, ts);   // candidate scan + b2TimeOfImpact of every candidate (the slowest thread's)
+            const unsigned long long te = MRP_NOW();
             MRP_PROG(0x2800u + pass);
             if (tid == 0) { sh.toi_solve = 0; toi_event(dt); }
             __syncthreads();
@@ -2568,8 +2571,9 @@ template <int ENV> struct World {
                 __syncthreads();
             }
             MRP_PROG(0x2c00u + pass);
-            if (sh.toi_done) break;
+            if (sh.toi_done) { MRP_SUB(21, te); break; }
             if (sh.toi_fnc) find_new_contacts_coop();
+            MRP_SUB(21, te);   // the event: island, sub-step solve, FindNewContacts
         }
     }
 

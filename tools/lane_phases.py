@@ -77,8 +77,8 @@ def main():
                               "load_marks": [float(blk[:, 24].mean()), float(blk[:, 25].mean()), float(blk[:, 26].mean())],
                               # store sub-phases: outputs + barrier, LaneState write-back (cycles)
                               "store_split": [float(blk[:, 22].mean()), float(blk[:, 23].mean())],
-                              # entry probes: 256 s_nop of straight-line code, one load of the state's cHW word
-                              "probe_ifetch_1kb": float(blk[:, 20].mean()), "probe_first_load": float(blk[:, 21].mean()),
+                              # TOI split: candidate scan + b2TimeOfImpact, events (cycles)
+                              "toi_split": [float(blk[:, 20].mean()), float(blk[:, 21].mean())],
                               "last_to_end_launches": int(last_block[k])})
         p = res["blocks"][-1]["mean_phases"]
         print(f"lanes {k * 1024:5d}-{min(lanes, (k + 1) * 1024) - 1:5d}: slowest in {slow_block[k]:2d}/{steps} launches, "
@@ -86,7 +86,7 @@ def main():
               f"mean total {blk[:, 11].mean():9.0f}  load {p['load+act']:8.0f}  solve {p['solve(islands)']:8.0f}  "
               f"TOI {p['TOI']:8.0f}  store {p['store']:8.0f} (outputs {blk[:, 22].mean():7.0f} write-back {blk[:, 23].mean():7.0f})  load marks "
               + " ".join(f"{v:8.0f}" for v in res["blocks"][-1]["load_marks"])
-              + f"  probes: 1 KB code {blk[:, 20].mean():7.0f} first load {blk[:, 21].mean():7.0f}")
+              + f"  TOI split {blk[:, 20].mean():7.0f} / {blk[:, 21].mean():7.0f}")
     if out:
         with open(out, "w") as f:
             json.dump(res, f, indent=1)

@@ -22,7 +22,7 @@ NAMES = ["load+act", "apply_actions", "FNC(new fixtures)", "collide", "solve(isl
          "TOI", "obs/reward", "outputs", "auto-reset", "store"]
 # trace words: 0-10 phases, 11 total, 12 island contacts, 13 TOI events, 14 position passes, 15 velocity
 # updates run, 16 velocity-sweep cycles, 17 position-pass cycles, 18 island set-up cycles (thread 0),
-# 19 largest island's contact count, 20-23 its first contacts' bodies (A << 8 | B)
+# 19 largest island's contact count, 20/21 TOI split (scan + b2TimeOfImpact, events), 22/23 store split
 SUB = {"velocity_sweeps": 16, "position_passes": 17, "island_setup": 18}
 
 
@@ -69,7 +69,10 @@ def main():
                "solve_split_cycles_mean": {k: float(slow[:, w].mean()) for k, w in SUB.items()},
                "island_contacts_mean": float(slow[:, 12].mean()), "toi_events_mean": float(slow[:, 13].mean()),
                "position_passes_mean": float(slow[:, 14].mean()), "velocity_updates_mean": float(slow[:, 15].mean()),
-               "largest_island_contacts_mean": float(slow[:, 19].mean())},
+               "largest_island_contacts_mean": float(slow[:, 19].mean()),
+               # TOI phase split: candidate scan + b2TimeOfImpact of every candidate, then the events
+               # (TOI island, sub-step solve, FindNewContacts)
+               "toi_split_cycles_mean": {"scan_and_time_of_impact": float(slow[:, 20].mean()), "events": float(slow[:, 21].mean())}},
            "ten_slowest_lanes_per_launch": {
                "total_cycles_mean": float(slow10[:, 11].mean()),
                "phases_cycles_mean": {n: float(slow10[:, i].mean()) for i, n in enumerate(NAMES)},
@@ -83,6 +86,8 @@ def main():
         print(f"  {n:20s} {res['mean_lane_step_phases'][n]:10.0f} {v:10.0f} {100 * v / s['total_cycles_mean']:5.1f}%")
     for k, v in s["solve_split_cycles_mean"].items():
         print(f"    solve: {k:16s} {v:10.0f} {100 * v / s['total_cycles_mean']:5.1f}%")
+    t = s["toi_split_cycles_mean"]
+    print(f"    TOI: scan + b2TimeOfImpact {t['scan_and_time_of_impact']:10.0f}, events {t['events']:10.0f}")
     print(f"  slowest lane: island contacts {s['island_contacts_mean']:.2f}, velocity updates {s['velocity_updates_mean']:.0f}, "
           f"position passes {s['position_passes_mean']:.1f}, TOI events {s['toi_events_mean']:.2f}")
     if out:
