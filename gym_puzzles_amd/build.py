@@ -37,7 +37,12 @@ DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("mrp_math.h", "mrp_config.h", 
 _MAX_ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
 _ILP_LOOPS = ["-DMRP_SOLVE_NOINLINE_LANES"] + _MAX_ILP
 _LANES_PAIRS = ["-DMRP_LANES_PAIRS=1"]
-UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS, "mrp_env1.hip": _MAX_ILP, "mrp_env4.hip": _ILP_LOOPS, "mrp_env5.hip": _LANES_PAIRS}
+# v2 moves its live contact slots in 16-B granules (-DMRP_CONTACT_GRANULES=1): +2.5 % at the same
+# traffic; for v0 / v3 the granules measured level in time and +16 % in traffic, so they move words
+# (profiles/r4_ab_contact_granules.txt).
+_GRANULES = ["-DMRP_CONTACT_GRANULES=1"]
+UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS, "mrp_env1.hip": _MAX_ILP, "mrp_env2.hip": _GRANULES, "mrp_env4.hip": _ILP_LOOPS,
+              "mrp_env5.hip": _LANES_PAIRS}
 # -fno-slp-vectorize: the serial solver chains are latency-bound; packing pairs of f32 ops into
 # v_pk_* costs operand-shuffling moves on the dependency chain (measured +2-3 % env-steps/s off)
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",

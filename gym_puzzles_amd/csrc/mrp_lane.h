@@ -14,6 +14,7 @@
 
 #include <cstddef>
 #include <cstring>
+#include <type_traits>
 
 #include "mrp_env.h"
 #include "mrp_ops.h"
@@ -128,11 +129,12 @@ struct StateIO {
     static constexpr int HWW = (int)(offsetof(LS, cHW) / 4);
     static_assert(Q - P == LS::NCA * C, "contact arrays cnext .. mid[1] are contiguous");
     // The contact slots' words [P, Q): NCA arrays of C words, slot c of array a at word
-    // P + a * C + c; only slots below the mark hw are live and move (word by word: moving whole
-    // 16-B granules of the live runs measured the same time and 23 % more PMC traffic for v0).
+    // P + a * C + c; only slots below the mark hw are live and move, word by word (ContactWords) or
+    // in 16-B granules (ContactGranules, MRP_CONTACT_GRANULES=1: the v2 unit, +2.5 % there; for v0
+    // and v3 level in time and +16 % in PMC traffic, profiles/r4_ab_contact_granules.txt).
     // The load issues every live word's load before the first wait and puts the initial contents
     // into the other words.
-    struct Contacts {
+    struct ContactWords {
         static constexpr int NWC = LS::NCA * C, NK = (NWC + BLOCK - 1) / BLOCK;
         word_t w[NK];
         __device__ __forceinline__ static bool live(int i, int hw) { return i % C < hw; }   // i: word of the region
@@ -162,6 +164,67 @@ struct StateIO {
             }
         }
     };
+    // The same words moved in 16-B granules: a granule with any live word moves whole; its other
+    // words hold their initial contents on both sides (in HBM by the cHW invariant, in LDS because
+    // the load puts them there and the step takes slots only at the mark), and the load replaces
+    // them by those contents word by word (MRP_CONTACT_GRANULES=1: fewer, wider loads, more traffic)
+    struct ContactGranules {
+        static constexpr int QA = (P + 3) / 4, QB = Q / 4, NQ = (QB - QA + BLOCK - 1) / BLOCK;
+        static constexpr int H = 4 * QA - P, T = Q - 4 * QB;
+        static_assert(QA < QB && H + T < BLOCK, "contact words span whole granules");
+        quad_t q[NQ];
+        word_t s;
+        __device__ __forceinline__ static bool live(int w, int hw) { return (w - P) % C < hw; }
+        __device__ __forceinline__ static word_t init(int w) {
+            const int i = w - P;   // cnext (array 0) chains the free list 0 -> 1 -> ... -> C-1; the rest are 0
+            return i < C ? (i + 1 < C ? (word_t)(i + 1) : (word_t)NULLN) : 0u;
+        }
+        // granule j's first slot; its words are slots c0 .. c0 + 3, wrapping into the next array's
+        // slots 0, 1, 2 (C >= 4), so it is live iff c0 < hw or it wraps and slot 0 is live
+        __device__ __forceinline__ static int slot0(int j) { return (4 * j - P) % C; }
+        __device__ __forceinline__ static bool quad_live(int c0, int hw) { return (c0 < hw) | ((c0 + 3 >= C) & (hw > 0)); }
+        __device__ __forceinline__ static word_t pick(word_t v, int c, int w, int hw) {
+            return (c >= C ? c - C : c) < hw ? v : init(w);
+        }
+        static_assert(C >= 4, "a granule spans at most two arrays");
+        __device__ __forceinline__ static int single(int tid) { return tid < H ? P + tid : 4 * QB + (tid - H); }
+        __device__ __forceinline__ void issue(const word_t* g, int hw, int tid) {
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) {
+                const int j = QA + tid + k * BLOCK;
+                if ((j < QB) & quad_live(slot0(j), hw)) q[k] = reinterpret_cast<const quad_t*>(g)[j];
+            }
+            if ((tid < H + T) & live(single(tid), hw)) s = g[single(tid)];
+        }
+        __device__ __forceinline__ void put(word_t* lds, int hw, int tid) const {
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) {
+                const int j = QA + tid + k * BLOCK;
+                if (j < QB) {
+                    const int c0 = slot0(j);
+                    quad_t v = q[k];
+                    v.x = pick(v.x, c0, 4 * j, hw);
+                    v.y = pick(v.y, c0 + 1, 4 * j + 1, hw);
+                    v.z = pick(v.z, c0 + 2, 4 * j + 2, hw);
+                    v.w = pick(v.w, c0 + 3, 4 * j + 3, hw);
+                    reinterpret_cast<quad_t*>(lds)[j] = v;
+                }
+            }
+            if (tid < H + T) lds[single(tid)] = live(single(tid), hw) ? s : init(single(tid));
+        }
+        __device__ __forceinline__ static void store(const word_t* lds, word_t* g, int hw, int tid) {
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) {
+                const int j = QA + tid + k * BLOCK;
+                if ((j < QB) & quad_live(slot0(j), hw)) reinterpret_cast<quad_t*>(g)[j] = reinterpret_cast<const quad_t*>(lds)[j];
+            }
+            if ((tid < H + T) & live(single(tid), hw)) g[single(tid)] = lds[single(tid)];
+        }
+    };
+#ifndef MRP_CONTACT_GRANULES
+#define MRP_CONTACT_GRANULES 0
+#endif
+    using Contacts = typename std::conditional<MRP_CONTACT_GRANULES != 0, ContactGranules, ContactWords>::type;
     // hw_io <- the loaded cHW (clamped to the pool; kept in LDS, not live in registers across the step)
     __device__ __forceinline__ static void load(LS& S, int& hw_io, const uint32_t* __restrict__ gs, int lane, int tid) {
         const word_t* g = gs + (size_t)lane * NW;
