@@ -426,16 +426,7 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_step(uint32_t*
         for (int k = tid; k < D::OBS; k += BLOCK) obs[row * D::OBS + k] = sh.obs[k];
         __syncthreads();
     }
-#ifdef MRP_STAMPS
-    // store sub-stamps (words 22 / 23 replace the island-body diagnostics here): outputs + barrier,
-    // then the LaneState write-back
-    unsigned long long st0 = 0;
-    if (tid == 0) { st0 = __builtin_amdgcn_s_memtime(); sh.trace[22] = (uint32_t)(st0 - sh.stamp_t); }
-#endif
     StateIO<ENV>::store(sh.S, sh.hw_io, state, lane, tid);
-#ifdef MRP_STAMPS
-    if (tid == 0) sh.trace[23] = (uint32_t)(__builtin_amdgcn_s_memtime() - st0);
-#endif
     if (cost && tid == 0) cost[lane] = (uint32_t)min(__builtin_amdgcn_s_memtime() - t_start, 0xffffffffull);
     MRP_STAMP(10);
 #ifdef MRP_STAMPS

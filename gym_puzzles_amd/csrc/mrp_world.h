@@ -50,6 +50,11 @@ constexpr int NULLN = -1;
 // constants in VGPRs; inlined into k_step they pushed its VGPR spills from 9 to 85.  As functions of
 // their own they get the register file to themselves (k_step saves its live registers around the one
 // call per island solve, not per sweep).  MRP_XW_INLINE (A/B) inlines them.
+// MRP_COLLIDE_GROUPS (default 1): the narrow phase of up to 32 contacts on groups of 8 / 4 / 2 lanes
+// per contact (round 4 A/B, profiles/r4_ab_collide_groups.txt: v2 +4.3 %, v3 +0.6 / +1.7 %, v0 +0.2 / +0.9 %)
+#ifndef MRP_COLLIDE_GROUPS
+#define MRP_COLLIDE_GROUPS 1
+#endif
 // MRP_LANES_PAIRS=1: the lanes-path sweeps two per loop trip (lanes_sweeps; build.py sets it for the
 // v0 and v3 units, where it measured faster)
 #ifndef MRP_LANES_PAIRS
@@ -83,7 +88,7 @@ constexpr int MRP_TRACE_W = 32;
 static __device__ uint32_t g_trace[16384][MRP_TRACE_W];   // last step per lane: phases 0-10, total, nc, toi, pos, vel-units,
                                                        // velocity / position / island-set-up cycles, largest island,
                                                        // 20/21 TOI split (candidate scan + b2TimeOfImpact, events),
-                                                       // 22/23 store sub-phases (outputs, write-back), 24-26 load
+                                                       // 22/23 collide split (narrow phase, serial commit), 24-26 load
                                                        // sub-phases (state, tables, barrier), 27 step index mod 256,
                                                        // 28/29 s_memrealtime at entry / end, 30/31 HW_ID / XCC_ID
 #define MRP_NOW() __builtin_amdgcn_s_memtime()
@@ -622,6 +627,31 @@ template <int ENV> struct World {
         edge = best;
         return maxSep;
     }
+    // find_max_separation over a group of G lanes (G a power of two <= 8; the group's lanes are
+    // consecutive and `sub` is this lane's place in it): lane sub scans edges sub, sub + G, ... in
+    // the reference's order and rule (strict >, so the first index of the maximum wins), then the
+    // group reduces to the larger separation, the smaller edge among equals.  An edge that never
+    // beats the reference's running maximum (NaN, or not above -FLT_MAX) takes no part; with none
+    // left the result is the reference's (edge 0, -FLT_MAX).  Same bits as find_max_separation.
+    __device__ __forceinline__ static float find_max_separation_grp(int& edge, const ShapeDef& p1, Xf x1, const ShapeDef& p2, Xf x2,
+                                                                    int sub, int G) {
+        Xf x = mulT_xx(x2, x1);
+        int best = MAX_POLY; float maxSep = -FLT_MAXV;
+        for (int i = sub; i < p1.count; i += G) {
+            V2 n = mul_rv(x.q, p1.n[i]);
+            V2 v1 = mul_xv(x, p1.v[i]);
+            float si = FLT_MAXV;
+            for (int j = 0; j < p2.count; ++j) { float sij = vdot(n, vsub(p2.v[j], v1)); if (sij < si) si = sij; }
+            if (si > maxSep) { maxSep = si; best = i; }
+        }
+        for (int m = 1; m < G; m <<= 1) {
+            const float os = __shfl_xor(maxSep, m, G);
+            const int ob = __shfl_xor(best, m, G);
+            if (ob < MAX_POLY && (best == MAX_POLY || os > maxSep || (os == maxSep && ob < best))) { maxSep = os; best = ob; }
+        }
+        edge = best == MAX_POLY ? 0 : best;
+        return best == MAX_POLY ? -FLT_MAXV : maxSep;
+    }
     // b2ClipSegmentToLine with the two in/out vertices kept in registers
     __device__ __forceinline__ static int clip(ClipV& o0, ClipV& o1, const ClipV& i0, const ClipV& i1, V2 normal, float offset, int vertexIndexA) {
         int numOut = 0;
@@ -647,15 +677,16 @@ template <int ENV> struct World {
     __device__ __forceinline__ float& m_px(int i, int k) { return k < 0 ? sh.spx[i] : sh.u.col.tpx[i][k]; }
     __device__ __forceinline__ float& m_py(int i, int k) { return k < 0 ? sh.spy[i] : sh.u.col.tpy[i][k]; }
     __device__ __forceinline__ uint32_t& m_id(int i, int k) { return k < 0 ? sh.smid[i] : sh.u.col.tmid[i][k]; }
-    // b2CollidePolygons into manifold scratch slot k
-    __device__ __forceinline__ void collide_polygons(int k, const ShapeDef& pA, Xf xA, const ShapeDef& pB, Xf xB) {
+    // b2CollidePolygons into manifold scratch slot k; with G > 1 the G lanes of a group run it
+    // together (find_max_separation_grp), every lane computing the same values for the rest
+    __device__ __forceinline__ void collide_polygons(int k, const ShapeDef& pA, Xf xA, const ShapeDef& pB, Xf xB, int sub = 0, int G = 1) {
         m_pc(k) = 0;
         float totalRadius = pA.radius + pB.radius;
         int edgeA = 0;
-        float sepA = find_max_separation(edgeA, pA, xA, pB, xB);
+        float sepA = G > 1 ? find_max_separation_grp(edgeA, pA, xA, pB, xB, sub, G) : find_max_separation(edgeA, pA, xA, pB, xB);
         if (sepA > totalRadius) return;
         int edgeB = 0;
-        float sepB = find_max_separation(edgeB, pB, xB, pA, xA);
+        float sepB = G > 1 ? find_max_separation_grp(edgeB, pB, xB, pA, xA, sub, G) : find_max_separation(edgeB, pB, xB, pA, xA);
         if (sepB > totalRadius) return;
         const float k_tol = 0.1f * LINEAR_SLOP;
         bool flip = sepB > sepA + k_tol;
@@ -746,6 +777,7 @@ template <int ENV> struct World {
     // run the broad-phase overlap test + SAT narrow phase of one contact each, then thread 0
     // destroys / commits in list order (events fire in the reference's order).
     __device__ __forceinline__ void collide_coop() {
+        const unsigned long long tc0 = MRP_NOW();
         if (tid == 0) {
             int n = 0;
             for (int c = S.cHead, g_ = 0; c != NULLN && list_ok(g_); c = S.cnext[c]) sh.clist[n++] = c;
@@ -753,12 +785,26 @@ template <int ENV> struct World {
         }
         __syncthreads();
         const int n = sh.ccount;
-        for (int i = tid; i < n; i += 64) {
-            int c = sh.clist[i];
-            int fa = S.cfa[c], fb = S.cfb[c];
-            bool ov = fat_overlap(S.proxy[fa], S.proxy[fb]);
-            sh.cover[i] = ov ? 1 : 0;
-            if (ov) collide_polygons(i, L.shape[fa], xf(L.fix_body[fa]), L.shape[fb], xf(L.fix_body[fb]));
+        // up to 32 contacts: a group of G = 8, 4 or 2 lanes per contact shares its SAT edge scans
+        // (collide_polygons with G > 1); more: one lane per contact
+        const int G = MRP_COLLIDE_GROUPS ? (n <= 8 ? 8 : (n <= 16 ? 4 : (n <= 32 ? 2 : 1))) : 1;
+        if (G > 1) {
+            const int g = tid / G, sub = tid & (G - 1);
+            if (g < n) {
+                int c = sh.clist[g];
+                int fa = S.cfa[c], fb = S.cfb[c];
+                bool ov = fat_overlap(S.proxy[fa], S.proxy[fb]);
+                if (sub == 0) sh.cover[g] = ov ? 1 : 0;
+                if (ov) collide_polygons(g, L.shape[fa], xf(L.fix_body[fa]), L.shape[fb], xf(L.fix_body[fb]), sub, G);
+            }
+        } else {
+            for (int i = tid; i < n; i += 64) {
+                int c = sh.clist[i];
+                int fa = S.cfa[c], fb = S.cfb[c];
+                bool ov = fat_overlap(S.proxy[fa], S.proxy[fb]);
+                sh.cover[i] = ov ? 1 : 0;
+                if (ov) collide_polygons(i, L.shape[fa], xf(L.fix_body[fa]), L.shape[fb], xf(L.fix_body[fb]));
+            }
         }
         // touching contacts after this update decide how much solver work the lane has left: the
         // contact-heavy lanes set the kernel's duration, so they take issue priority from here on
@@ -774,6 +820,8 @@ template <int ENV> struct World {
         if (prio_floor > step_prio) step_prio = prio_floor;
         set_prio(step_prio);
         __syncthreads();
+        MRP_SUB(22, tc0);   // collide split: contact-list snapshot + narrow phase of every contact
+        const unsigned long long tc1 = MRP_NOW();
         if (tid == 0) {
             for (int i = 0; i < n; ++i) {
                 int c = sh.clist[i];
@@ -782,6 +830,7 @@ template <int ENV> struct World {
             }
         }
         __syncthreads();
+        MRP_SUB(23, tc1);   // collide split: serial commit (feature-id matching, events, destroys)
     }
 
     // wave issue priority (s_setprio takes an immediate); `level` must be wave-uniform

@@ -75,8 +75,8 @@ def main():
                               "mean_phases": {n: float(blk[:, i].mean()) for i, n in enumerate(NAMES)},
                               # load sub-phases, cycles from the wave's start: state loaded, tables loaded, barrier
                               "load_marks": [float(blk[:, 24].mean()), float(blk[:, 25].mean()), float(blk[:, 26].mean())],
-                              # store sub-phases: outputs + barrier, LaneState write-back (cycles)
-                              "store_split": [float(blk[:, 22].mean()), float(blk[:, 23].mean())],
+                              # collide split: narrow phase, serial commit (cycles)
+                              "collide_split": [float(blk[:, 22].mean()), float(blk[:, 23].mean())],
                               # TOI split: candidate scan + b2TimeOfImpact, events (cycles)
                               "toi_split": [float(blk[:, 20].mean()), float(blk[:, 21].mean())],
                               "last_to_end_launches": int(last_block[k])})
@@ -84,7 +84,7 @@ def main():
         print(f"lanes {k * 1024:5d}-{min(lanes, (k + 1) * 1024) - 1:5d}: slowest in {slow_block[k]:2d}/{steps} launches, "
               f"last to end in {last_block[k]:2d}, "
               f"mean total {blk[:, 11].mean():9.0f}  load {p['load+act']:8.0f}  solve {p['solve(islands)']:8.0f}  "
-              f"TOI {p['TOI']:8.0f}  store {p['store']:8.0f} (outputs {blk[:, 22].mean():7.0f} write-back {blk[:, 23].mean():7.0f})  load marks "
+              f"TOI {p['TOI']:8.0f}  store {p['store']:8.0f} (collide: narrow {blk[:, 22].mean():7.0f} commit {blk[:, 23].mean():7.0f})  load marks "
               + " ".join(f"{v:8.0f}" for v in res["blocks"][-1]["load_marks"])
               + f"  TOI split {blk[:, 20].mean():7.0f} / {blk[:, 21].mean():7.0f}")
     if out:

@@ -22,7 +22,7 @@ NAMES = ["load+act", "apply_actions", "FNC(new fixtures)", "collide", "solve(isl
          "TOI", "obs/reward", "outputs", "auto-reset", "store"]
 # trace words: 0-10 phases, 11 total, 12 island contacts, 13 TOI events, 14 position passes, 15 velocity
 # updates run, 16 velocity-sweep cycles, 17 position-pass cycles, 18 island set-up cycles (thread 0),
-# 19 largest island's contact count, 20/21 TOI split (scan + b2TimeOfImpact, events), 22/23 store split
+# 19 largest island's contact count, 20/21 TOI split (scan + b2TimeOfImpact, events), 22/23 collide split (narrow phase, commit)
 SUB = {"velocity_sweeps": 16, "position_passes": 17, "island_setup": 18}
 
 
@@ -72,7 +72,9 @@ def main():
                "largest_island_contacts_mean": float(slow[:, 19].mean()),
                # TOI phase split: candidate scan + b2TimeOfImpact of every candidate, then the events
                # (TOI island, sub-step solve, FindNewContacts)
-               "toi_split_cycles_mean": {"scan_and_time_of_impact": float(slow[:, 20].mean()), "events": float(slow[:, 21].mean())}},
+               "toi_split_cycles_mean": {"scan_and_time_of_impact": float(slow[:, 20].mean()), "events": float(slow[:, 21].mean())},
+               # collide split: contact-list snapshot + narrow phase of every contact, then thread 0's commit
+               "collide_split_cycles_mean": {"narrow_phase": float(slow[:, 22].mean()), "serial_commit": float(slow[:, 23].mean())}},
            "ten_slowest_lanes_per_launch": {
                "total_cycles_mean": float(slow10[:, 11].mean()),
                "phases_cycles_mean": {n: float(slow10[:, i].mean()) for i, n in enumerate(NAMES)},
@@ -88,6 +90,8 @@ def main():
         print(f"    solve: {k:16s} {v:10.0f} {100 * v / s['total_cycles_mean']:5.1f}%")
     t = s["toi_split_cycles_mean"]
     print(f"    TOI: scan + b2TimeOfImpact {t['scan_and_time_of_impact']:10.0f}, events {t['events']:10.0f}")
+    c = s["collide_split_cycles_mean"]
+    print(f"    collide: narrow phase {c['narrow_phase']:10.0f}, serial commit {c['serial_commit']:10.0f}")
     print(f"  slowest lane: island contacts {s['island_contacts_mean']:.2f}, velocity updates {s['velocity_updates_mean']:.0f}, "
           f"position passes {s['position_passes_mean']:.1f}, TOI events {s['toi_events_mean']:.2f}")
     if out:

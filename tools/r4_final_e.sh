@@ -1,0 +1,60 @@
+#!/bin/bash
+# Round-4 final evidence on the final library (collide groups, v2 contact granules), one call:
+# the GPU suite, smoke, the rocprofv3 set of every BASELINE config (kernel trace + stats,
+# FETCH_SIZE, WRITE_SIZE; profiles/pmc_traffic.json on the box), the issue-roofline capture /
+# replay and phase split of every config (stamps build) -> profiles/r4_issue_roofline.json on the
+# box, then the driver-window bench line of every config (reading both fresh tables) with its
+# like-for-like CPU baseline, the driver-window and default v0 lines, and the single-env timing.
+# The chain stops at the first failure.
+set -uo pipefail
+O=gpurun_out/r4fe
+mkdir -p $O
+( for i in $(seq 1 75); do date >> gpurun_out/heartbeat; sleep 20; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 \
+  || { echo "gpu tests failed"; tail -30 $O/gpu_tests.log; exit 1; }
+tail -1 $O/gpu_tests.log
+timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 \
+  || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+STEPS=20 WARMUP=5 LANES=4096 VALU_PMC=1 timeout -k 10 400 bash tools/profile.sh r4i_v0 0 > /dev/null || { echo "profile v0 failed"; exit 1; }
+STEPS=20 WARMUP=5 LANES=4096 timeout -k 10 400 bash tools/profile.sh r4i_heavy_v0 1 > /dev/null || { echo "profile 1 failed"; exit 1; }
+STEPS=20 WARMUP=5 LANES=1024 timeout -k 10 400 bash tools/profile.sh r4i_v2 2 > /dev/null || { echo "profile 2 failed"; exit 1; }
+STEPS=20 WARMUP=5 LANES=1024 timeout -k 10 400 bash tools/profile.sh r4i_heavy_v2_3block 4 > /dev/null || { echo "profile 4 failed"; exit 1; }
+STEPS=20 WARMUP=5 LANES=4096 timeout -k 10 400 bash tools/profile.sh r4i_v3 5 > /dev/null || { echo "profile 5 failed"; exit 1; }
+echo "profiles done"
+O2=gpurun_out/r4fe2
+mkdir -p $O2
+STAMPS=gym_puzzles_amd/libmrp_stamps.so
+for cfg in "0 4096" "1 4096" "2 1024" "4 1024" "5 4096"; do
+  set -- $cfg
+  MRP_LIB=$STAMPS timeout -k 10 200 python tools/issue_capture.py $1 $2 5 20 $O2/cap_env$1.npz > $O2/cap_env$1.log 2>&1 \
+    || { echo "capture $1 failed"; tail $O2/cap_env$1.log; exit 1; }
+  MRP_LIB=$STAMPS timeout -k 10 200 python tools/issue_replay.py $O2/cap_env$1.npz $O2/replay_stamps_env$1.json > $O2/replay_stamps_env$1.log 2>&1 \
+    || { echo "stamps replay $1 failed"; tail $O2/replay_stamps_env$1.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_VMEM SQ_WAVE_CYCLES \
+      --output-format csv -d $O2/pmc_env$1 -o pmc -- python3 tools/issue_replay.py $O2/cap_env$1.npz /tmp/r.json > $O2/pmc_env$1.log 2>&1 \
+    || { echo "pmc $1 failed"; tail $O2/pmc_env$1.log; exit 1; }
+  timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $O2/kt_env$1 -o kt -- python3 tools/issue_replay.py $O2/cap_env$1.npz /tmp/r.json 3 \
+      > $O2/kt_env$1.log 2>&1 || { echo "kt $1 failed"; tail $O2/kt_env$1.log; exit 1; }
+  MRP_LIB=$STAMPS timeout -k 10 200 python tools/phase_profile.py $1 $2 5 20 $O2/r4_phase_env$1.json > $O2/r4_phase_env$1.txt 2>&1 \
+    || { echo "phase $1 failed"; tail $O2/r4_phase_env$1.txt; exit 1; }
+  echo "env $1 captured"
+done
+python3 tools/issue_roofline.py $O2 profiles/r4_issue_roofline.json > $O2/issue_roofline.txt || { echo "issue roofline failed"; exit 1; }
+cp profiles/r4_issue_roofline.json $O2/
+for cfg in "0 4096" "1 4096" "2 1024" "4 1024" "5 4096"; do
+  set -- $cfg
+  timeout -k 10 300 python bench.py --env $1 --lanes $2 --steps 20 --warmup 5 --later-window 0 --episode 0 --multi-step 0 \
+      --single-env 0 > $O/cfg_env$1.log 2>&1 || { echo "bench env $1 failed"; tail -20 $O/cfg_env$1.log; exit 1; }
+  tail -1 $O/cfg_env$1.log | cut -c1-160
+done
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_driver.log 2>&1 || { echo "driver bench failed"; tail -20 $O/bench_driver.log; exit 1; }
+tail -1 $O/bench_driver.log | cut -c1-200
+timeout -k 10 300 python bench.py > $O/bench_default.log 2>&1 || { echo "default bench failed"; tail -20 $O/bench_default.log; exit 1; }
+tail -1 $O/bench_default.log | cut -c1-160
+timeout -k 10 200 python tools/single_env_timing.py MultiRobotPuzzle-v0 300 > $O2/single_env.log 2>&1 || { echo "single env failed"; tail $O2/single_env.log; exit 1; }
+cat $O2/single_env.log
+exit 0
