@@ -1,0 +1,110 @@
+"""Host restatements of two round-4 exactness arguments (CPU only; the device code itself is
+covered bit for bit against the oracle by tests/test_gpu.py).
+
+1. The grouped SAT edge scan (mrp_world.h find_max_separation_grp): G lanes each scan edges
+   sub, sub + G, ... with the reference's strict-greater rule, then reduce pairwise (larger
+   separation, smaller edge among equals; an edge that never beat -FLT_MAX or is NaN takes no
+   part).  Must give the reference's sequential b2FindMaxSeparation result for any values.
+2. The sparse early-exit schedule (mrp_world.h exit_mask / Snap::step, sweep_pairs, lanes_sweeps):
+   every compare point k has a snapshot from exactly two sweeps before and iters - k even, so a
+   repeat found there gives the state after all `iters` sweeps.
+"""
+import itertools
+import math
+import random
+import struct
+
+import pytest
+
+FLT_MAX = 3.4028234663852886e38
+MAX_POLY = 8
+
+
+def f32(x):
+    return struct.unpack("f", struct.pack("f", x))[0]
+
+
+def bits(x):
+    return struct.pack("f", x)
+
+
+def sequential(vals):   # b2FindMaxSeparation's edge loop (mrp_world.h find_max_separation)
+    best, max_sep = 0, -FLT_MAX
+    for i, v in enumerate(vals):
+        if v > max_sep:
+            max_sep, best = v, i
+    return best, max_sep
+
+
+def grouped(vals, G):   # find_max_separation_grp
+    lanes = []
+    for sub in range(G):
+        best, max_sep = MAX_POLY, -FLT_MAX
+        for i in range(sub, len(vals), G):
+            if vals[i] > max_sep:
+                max_sep, best = vals[i], i
+        lanes.append([max_sep, best])
+    m = 1
+    while m < G:   # butterfly over xor masks, every lane updated from its partner's previous value
+        prev = [list(x) for x in lanes]
+        for sub in range(G):
+            os, ob = prev[sub ^ m]
+            ms, b = prev[sub]
+            if ob < MAX_POLY and (b == MAX_POLY or os > ms or (os == ms and ob < b)):
+                lanes[sub] = [os, ob]
+        m <<= 1
+    out = set()
+    for ms, b in lanes:
+        out.add((0 if b == MAX_POLY else b, bits(-FLT_MAX if b == MAX_POLY else ms)))
+    assert len(out) == 1, "every lane of the group must hold the same result"
+    return out.pop()
+
+
+POOL = [f32(x) for x in (0.0, -0.0, 1.5, -1.5, 2.0, -FLT_MAX, FLT_MAX, math.inf, -math.inf, 0.25, -0.25)] + [math.nan]
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_grouped_edge_scan_equals_sequential(G):
+    rng = random.Random(1234 + G)
+    for _ in range(20000):
+        n = rng.randint(1, MAX_POLY)
+        vals = [rng.choice(POOL) for _ in range(n)]
+        b, s = sequential(vals)
+        assert grouped(vals, G) == (b, bits(s)), vals
+
+
+def test_grouped_edge_scan_exhaustive_small():
+    small = [f32(0.0), f32(-0.0), f32(1.0), -FLT_MAX, math.nan]
+    for n in range(1, 5):
+        for vals in itertools.product(small, repeat=n):
+            b, s = sequential(list(vals))
+            for G in (2, 4, 8):
+                assert grouped(list(vals), G) == (b, bits(s)), (vals, G)
+
+
+def exit_mask(done, dense=32, sparse=16):
+    return sparse - 1 if done > dense else 3
+
+
+@pytest.mark.parametrize("pairs", [False, True])
+def test_sparse_exit_schedule_is_exact(pairs):
+    """Every compare point has its snapshot exactly two sweeps earlier and an even remainder."""
+    for iters in range(1, 400):
+        snap_at = None
+        k0 = 0
+        if pairs and iters & 1:
+            k0 = 1                      # an odd count runs its first sweep alone
+        if (iters - k0) & 3 == 2:
+            snap_at = k0                # the start is a snapshot point
+        step = 2 if pairs else 1
+        k = k0
+        while k < iters:
+            k += step
+            if not pairs and (iters - k) & 1:
+                continue                # the single-sweep loops check only at even remainders
+            left, m = iters - k, exit_mask(k)
+            if left & m == 0 and snap_at is not None:
+                assert k - snap_at == 2, (iters, k, snap_at)
+                assert (iters - k) % 2 == 0
+            if left & m == 2:
+                snap_at = k
