@@ -820,7 +820,9 @@ template <int ENV> struct World {
         if (prio_floor > step_prio) step_prio = prio_floor;
         set_prio(step_prio);
         __syncthreads();
+#ifndef MRP_STAMPS_TOI
         MRP_SUB(22, tc0);   // collide split: contact-list snapshot + narrow phase of every contact
+#endif
         const unsigned long long tc1 = MRP_NOW();
         if (tid == 0) {
             for (int i = 0; i < n; ++i) {
@@ -830,7 +832,9 @@ template <int ENV> struct World {
             }
         }
         __syncthreads();
+#ifndef MRP_STAMPS_TOI
         MRP_SUB(23, tc1);   // collide split: serial commit (feature-id matching, events, destroys)
+#endif
     }
 
     // wave issue priority (s_setprio takes an immediate); `level` must be wave-uniform
@@ -2596,6 +2600,10 @@ template <int ENV> struct World {
             MRP_PROG(0x2800u + pass);
             if (tid == 0) { sh.toi_solve = 0; toi_event(dt); }
             __syncthreads();
+#ifdef MRP_STAMPS_TOI   // words 22 / 23: the event's thread-0 set-up, its sub-step solve (-DMRP_STAMPS -DMRP_STAMPS_TOI)
+            MRP_SUB(22, te);
+            const unsigned long long tsv = MRP_NOW();
+#endif
             if (sh.toi_solve) {
                 const int nc = __builtin_amdgcn_readfirstlane(sh.isl.nc);
                 if (nc <= 64) {
@@ -2616,6 +2624,9 @@ template <int ENV> struct World {
                 }
                 else if (tid == 0) for (int i = 0; i < 180; ++i) solver_velocity(sh.isl, sh.u.sol.vcs);
                 __syncthreads();
+#ifdef MRP_STAMPS_TOI
+                MRP_SUB(23, tsv);
+#endif
                 if (tid == 0) toi_event_post();
                 __syncthreads();
             }
