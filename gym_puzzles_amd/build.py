@@ -40,8 +40,11 @@ _LANES_PAIRS = ["-DMRP_LANES_PAIRS=1"]
 # v2 moves its live contact slots in 16-B granules (-DMRP_CONTACT_GRANULES=1): +2.5 % at the same
 # traffic; for v0 / v3 the granules measured level in time and +16 % in traffic, so they move words
 # (profiles/r4_ab_contact_granules.txt).
+# v2 also takes the max-ilp scheduler on its inlined k_step (+3.2 % in the driver window, +3.0 % at
+# steps 21-220; on v0 -0.2 % and on v3 -1.5 %, so those keep the default scheduler;
+# profiles/r4_ab_max_ilp.txt).
 _GRANULES = ["-DMRP_CONTACT_GRANULES=1"]
-UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS, "mrp_env1.hip": _MAX_ILP, "mrp_env2.hip": _GRANULES, "mrp_env4.hip": _ILP_LOOPS,
+UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS, "mrp_env1.hip": _MAX_ILP, "mrp_env2.hip": _GRANULES + _MAX_ILP, "mrp_env4.hip": _ILP_LOOPS,
               "mrp_env5.hip": _LANES_PAIRS}
 # -fno-slp-vectorize: the serial solver chains are latency-bound; packing pairs of f32 ops into
 # v_pk_* costs operand-shuffling moves on the dependency chain (measured +2-3 % env-steps/s off)
