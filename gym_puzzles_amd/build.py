@@ -44,8 +44,12 @@ _LANES_PAIRS = ["-DMRP_LANES_PAIRS=1"]
 # steps 21-220; on v0 -0.2 % and on v3 -1.5 %, so those keep the default scheduler;
 # profiles/r4_ab_max_ilp.txt).
 _GRANULES = ["-DMRP_CONTACT_GRANULES=1"]
-UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS, "mrp_env1.hip": _MAX_ILP, "mrp_env2.hip": _GRANULES + _MAX_ILP, "mrp_env4.hip": _ILP_LOOPS,
-              "mrp_env5.hip": _LANES_PAIRS}
+# v0 and v3 run under LLVM's iterative-ilp scheduler: v0 +4.4 % in the driver window and +4.8 % at
+# steps 21-220, v3 +4.9 % / +4.4 %; Heavy-v0 -2 %, the 3-block config -1.7 % and v2 -2.5 % (against
+# max-ilp) under it, so those keep their choices (profiles/r4_ab_sched_iterative_ilp.txt).
+_ITER_ILP = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
+UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS + _ITER_ILP, "mrp_env1.hip": _MAX_ILP, "mrp_env2.hip": _GRANULES + _MAX_ILP,
+              "mrp_env4.hip": _ILP_LOOPS, "mrp_env5.hip": _LANES_PAIRS + _ITER_ILP}
 # -fno-slp-vectorize: the serial solver chains are latency-bound; packing pairs of f32 ops into
 # v_pk_* costs operand-shuffling moves on the dependency chain (measured +2-3 % env-steps/s off)
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
