@@ -46,10 +46,10 @@ EXPORTED = (
     "mrp_env_dims", "mrp_create", "mrp_destroy", "mrp_last_error", "mrp_n_lanes", "mrp_env_id",
     "mrp_set_stream", "mrp_synchronize", "mrp_set_reward_params", "mrp_update_params", "mrp_update_goal",
     "mrp_reset", "mrp_reset_device", "mrp_step", "mrp_step_device", "mrp_step_ex", "mrp_step_device_ex",
-    "mrp_step_n_device", "mrp_set_auto_reset", "mrp_set_frameskip", "mrp_set_seed", "mrp_set_schedule",
+    "mrp_step_n_device", "mrp_set_auto_reset", "mrp_set_frameskip", "mrp_set_seed", "mrp_set_schedule", "mrp_get_schedule",
     "mrp_get_bodies", "mrp_get_flags", "mrp_get_faults", "mrp_counters", "mrp_counters_ex", "mrp_state_words", "mrp_get_state", "mrp_set_state",
     "mrp_set_time_limit", "mrp_selftest_sincos", "mrp_debug_stamps", "mrp_debug_stamps_ext",
-    "mrp_debug_trace", "mrp_debug_progress", "mrp_debug_velbench", "mrp_norm_create", "mrp_norm_destroy", "mrp_norm_last_error", "mrp_norm_set_stream",
+    "mrp_debug_trace", "mrp_debug_trace_words", "mrp_debug_progress", "mrp_debug_velbench", "mrp_norm_create", "mrp_norm_destroy", "mrp_norm_last_error", "mrp_norm_set_stream",
     "mrp_norm_set_training", "mrp_norm_set_norm_obs", "mrp_norm_reset_device", "mrp_norm_step_device", "mrp_norm_step_device_ex", "mrp_norm_get_stats", "mrp_norm_set_stats",
     "mrp_render", "mrp_render_device", "mrp_get_goals", "mrp_shapes",
 )
@@ -94,6 +94,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.mrp_step_n_device.argtypes = [P, i, P, P, P, P, P, P, P, P]
     L.mrp_set_seed.argtypes = [P, u64]
     L.mrp_set_schedule.argtypes = [P, i]
+    L.mrp_get_schedule.argtypes = [P]
     L.mrp_set_auto_reset.argtypes = [P, i]
     L.mrp_set_frameskip.argtypes = [P, i]
     L.mrp_get_bodies.argtypes = [P, P]
@@ -128,10 +129,17 @@ def load(path: str | None = None) -> ctypes.CDLL:
     # their -D builds), so an A/B library must be built from this ABI too: a missing symbol raises here
     L.mrp_debug_stamps_ext.argtypes = [i, P, P, P]
     L.mrp_debug_trace.argtypes = [i, P, i]
+    L.mrp_debug_trace_words.argtypes = []
     L.mrp_debug_progress.argtypes = [i, ctypes.POINTER(P), i]
     L.mrp_debug_velbench.argtypes = [i, i, i, i, i, P]
     _lib = L
     return L
+
+
+def trace_words() -> int:
+    """Words per lane of mrp_debug_trace's rows (include/mrp.h MRP_TRACE_WORDS): size trace buffers
+    from this, never from a literal, so a tool cannot overrun its buffer when the row grows."""
+    return int(load().mrp_debug_trace_words())
 
 
 def env_dims(env_id: int) -> dict:
@@ -267,6 +275,11 @@ class Batch:
         """Lane scheduling (mrp_set_schedule): 0 off, 1 costliest-first dispatch, 2 issue priority
         from the previous step's cost, 3 both (True = 1); results are identical in every mode."""
         self._check(load().mrp_set_schedule(self._h, int(mode)))
+
+    def get_schedule(self) -> int:
+        """The lane scheduling mode in force (mrp_get_schedule): mrp_create's per-env default until
+        set_schedule is called."""
+        return int(load().mrp_get_schedule(self._h))
 
     def set_seed(self, seed: int):
         """Re-key the device RNG (later resets and synthetic actions); lanes, parameters, stream

@@ -443,6 +443,7 @@ int mrp_set_schedule(mrp_ctx* ctx, int costliest_first) {
     ctx->schedule = costliest_first;
     return MRP_OK;
 }
+int mrp_get_schedule(const mrp_ctx* ctx) { return ctx ? ctx->schedule : MRP_E_ARG; }
 
 int mrp_set_seed(mrp_ctx* ctx, uint64_t seed) {
     if (!ctx) return MRP_E_ARG;
@@ -615,16 +616,19 @@ int mrp_debug_stamps_ext(int device, uint64_t* pmax16, uint64_t* stepmax256, uin
     return rc;
 }
 
-// Diagnostic builds only: the last step's per-lane trace (n_lanes x 32 words, n_lanes <= 16384).
+// Diagnostic builds only: the last step's per-lane trace (n_lanes x MRP_TRACE_WORDS words,
+// n_lanes <= 16384).  The width is the stamps build's trace row (mrp_lane.h g_trace); callers size
+// their buffer from mrp_debug_trace_words() so the two cannot drift apart.
+int mrp_debug_trace_words(void) { return MRP_TRACE_WORDS; }
 int mrp_debug_trace(int device, uint32_t* out, int n_lanes) {
     if (!out || n_lanes <= 0 || n_lanes > 16384 || hipSetDevice(device) != hipSuccess) return MRP_E_ARG;
-    std::vector<uint32_t> tmp((size_t)n_lanes * 32);
-    std::memset(out, 0, tmp.size() * 4);
+    std::vector<uint32_t> tmp((size_t)n_lanes * MRP_TRACE_WORDS);
     int have = 0;
     for (int i = 0; i < N_ENVS; ++i) {   // only the unit that stepped has a non-zero trace
         hipError_t e = env_ops(i)->debug_read(DBG_TRACE, tmp.data(), tmp.size() * 4);
         if (e == hipErrorNotSupported) continue;
         if (e != hipSuccess) return MRP_E_HIP;
+        if (!have) std::memset(out, 0, tmp.size() * 4);   // the caller's buffer is written only by a stamps build
         ++have;
         for (size_t k = 0; k < tmp.size(); ++k) out[k] |= tmp[k];
     }

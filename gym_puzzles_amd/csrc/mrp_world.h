@@ -84,7 +84,7 @@ static __device__ unsigned long long g_stamps[16];     // per-phase sums over la
 static __device__ unsigned long long g_pmax[16];       // per-phase max over lane-steps
 static __device__ unsigned long long g_stepmax[256];   // per step (stepCounter mod 256): slowest lane's total
 static __device__ unsigned long long g_rt[2];          // sums of lane totals: s_memtime ticks, s_memrealtime ticks
-constexpr int MRP_TRACE_W = 32;
+constexpr int MRP_TRACE_W = 32;   // include/mrp.h MRP_TRACE_WORDS (static_assert in mrp_lane.h)
 static __device__ uint32_t g_trace[16384][MRP_TRACE_W];   // last step per lane: phases 0-10, total, nc, toi, pos, vel-units,
                                                        // velocity / position / island-set-up cycles, largest island,
                                                        // 20/21 TOI split (candidate scan + b2TimeOfImpact, events),

@@ -137,10 +137,15 @@ int mrp_set_frameskip(mrp_ctx* ctx, int frameskip);
  * lanes, parameters, stream or time limit: SB3 VecEnv.seed(seed) (train/train.py:63-75 seeds
  * every env before the first reset).  Per-lane streams stay keyed by the global lane index. */
 int mrp_set_seed(mrp_ctx* ctx, uint64_t seed);
-/* Lane scheduling (default off): each step dispatches the lanes in descending order of their
- * previous step's cost, so the long serial solver chains start first (one small sort kernel per
- * step).  Results never depend on it.  Measured 1-2 % slower on v0 at 4096 lanes. */
+/* Lane scheduling: with costliest_first = 1 each step dispatches the lanes in descending order of
+ * their previous step's cost, so the long serial solver chains start first (one small sort kernel
+ * per step); 0 keeps lane order.  Results never depend on it.  The default is per env id, set by
+ * mrp_create: on for Heavy-v0 (env 1) and v3 (env 5) when n_lanes exceeds the lanes k_step keeps
+ * resident at once (CUs x 4 SIMDs x its waves per SIMD), off otherwise (round-4 A/B, DESIGN.md:
+ * Heavy-v0 +4 %, v3 +1-2 %; v0 -0.9 % at 4096 lanes and -3..-5 % at 1024). */
 int mrp_set_schedule(mrp_ctx* ctx, int costliest_first);
+/* the context's current lane scheduling mode (the per-env default until mrp_set_schedule) */
+int mrp_get_schedule(const mrp_ctx* ctx);
 /* TimeLimit max_episode_steps applied inside mrp_step (default: the registered value of
  * gym_puzzles/__init__.py:6-27); 0 disables it (when an outer gym.wrappers.TimeLimit is used). */
 int mrp_set_time_limit(mrp_ctx* ctx, int max_episode_steps);
@@ -193,9 +198,13 @@ int mrp_debug_stamps(int device, uint64_t* out16);
  * (256 slots, indexed by step counter mod 256) and the (s_memtime, s_memrealtime) sums of lane
  * totals since the last call. */
 int mrp_debug_stamps_ext(int device, uint64_t* pmax16, uint64_t* stepmax256, uint64_t* rt2);
-/* Diagnostic builds only: the last step's per-lane trace, n_lanes x 24 words (phase cycles 0-10,
- * total, island contacts, TOI events, position iterations, velocity-solver contact units, then
- * velocity-sweep / position-pass / island set-up cycles and the largest island's contacts). */
+/* Diagnostic builds only: the last step's per-lane trace, n_lanes x MRP_TRACE_WORDS words (phase
+ * cycles 0-10, total, island contacts, TOI events, position iterations, velocity-solver contact
+ * units, velocity-sweep / position-pass / island set-up cycles, the TOI split (20-21), the collide
+ * split (22-23), then the lane timeline words).  `out` must hold n_lanes * mrp_debug_trace_words()
+ * words; it is left untouched (MRP_E_STATE) when the library has no diagnostic unit. */
+#define MRP_TRACE_WORDS 32
+int mrp_debug_trace_words(void);
 int mrp_debug_trace(int device, uint32_t* out, int n_lanes);
 /* Diagnostic builds (-DMRP_PROGRESS) only: allocate n_lanes host-mapped words that every lane's
  * thread 0 overwrites with the last progress point it reached; readable while a launch runs

@@ -1324,6 +1324,14 @@ static int period_scan(const float* hist, int ns, int iters) {
     return first;
 }
 
+/* The device's early-exit compare schedule (mrp_world.h exit_mask, MRP_EXIT_DENSE = 32 /
+ * MRP_EXIT_SPARSE = 16): after sweep `done` the state is compared with the snapshot of two sweeps
+ * earlier when (iters - done) & mask == 0 and snapshotted when it is 2.  One definition for the work
+ * model (the device sweep counts of tools/roofline_model.py) and the early-exit CPU port. */
+#define OR_EXIT_DENSE 32
+#define OR_EXIT_SPARSE 16
+static inline int exit_mask(int done) { return done > OR_EXIT_DENSE ? OR_EXIT_SPARSE - 1 : 3; }
+
 static int work_velocity_sweeps(Solver* s, int iters, int nbodies) {
     const int nc = s->count, ns = 4 * nc + 3 * nbodies;
     float* snap = (float*)malloc(sizeof(float) * (size_t)(ns > 0 ? ns : 1));
@@ -1348,12 +1356,12 @@ static int work_velocity_sweeps(Solver* s, int iters, int nbodies) {
         solver_solve_velocity(s);
         if (hist) WORK_STATE(hist + (size_t)(it + 1) * ns);
         if (run >= 0) continue;
-        const int left = iters - (it + 1);
-        if ((left & 3) == 0 && have) {
+        const int left = iters - (it + 1), m = exit_mask(it + 1);
+        if ((left & m) == 0 && have) {
             WORK_STATE(cur);
             if (memcmp(cur, snap, sizeof(float) * (size_t)ns) == 0) run = it + 1;
         }
-        if ((left & 3) == 2) { WORK_STATE(snap); have = 1; }
+        if ((left & m) == 2) { WORK_STATE(snap); have = 1; }
     }
 #undef WORK_STATE
     if (hist) {
@@ -1432,7 +1440,7 @@ static void velocity_sweeps(Solver* s, int iters, int nbodies) {
     for (int it = 0; it < iters; ++it) {
         solver_solve_velocity(s);
         /* the device's schedule (mrp_world.h exit_mask): every 4 sweeps up to sweep 32, then every 16 */
-        const int left = iters - (it + 1), m = it + 1 > 32 ? 15 : 3;
+        const int left = iters - (it + 1), m = exit_mask(it + 1);
         if ((left & m) == 0 && have) {
             SWEEP_STATE(cur);
             if (memcmp(cur, snap, sizeof(float) * (size_t)ns) == 0) break;

@@ -14,6 +14,10 @@
 #include <string.h>
 
 /* ---------------------------------------------------------------- Python float semantics */
+/* libm pow through a volatile pointer: gcc folds pow(x, 2.0) into x * x after inlining, but CPython's
+ * `x ** 2` is a real glibc pow call, which is not correctly rounded (<= 0.52 ulp) and differs from
+ * x * x in the last bit for rare inputs (found by tests/test_v2_env_layer.py's restatement) */
+static double (*volatile libm_pow)(double, double) = pow;
 /* CPython float_pow (Objects/floatobject.c) special cases, then libm pow */
 static double py_pow(double iv, double iw) {
     int negate = 0;
@@ -23,7 +27,7 @@ static double py_pow(double iv, double iw) {
     if (iv == 0.0) return iw > 0.0 ? (fmod(iw, 2.0) == 1.0 ? iv : 0.0) : INFINITY;
     if (iv < 0.0) { iv = -iv; negate = (fmod(fabs(iw), 2.0) == 1.0); }
     if (iv == 1.0) return negate ? -1.0 : 1.0;
-    double ix = pow(iv, iw);
+    double ix = libm_pow(iv, iw);
     return negate ? -ix : ix;
 }
 /* CPython float_rem / numpy npy_remainder: result carries the divisor's sign */

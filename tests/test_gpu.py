@@ -272,14 +272,21 @@ def test_step_device_with_torch_stream(gpu_lib):
     _eq("done", done.cpu().numpy(), h.done)
 
 
-def test_costliest_first_schedule_changes_nothing(gpu_lib):
+@pytest.mark.parametrize("env_id,lanes,explicit", [(0, 512, True), (1, 4096, False), (5, 4096, False)])
+def test_costliest_first_schedule_changes_nothing(gpu_lib, env_id, lanes, explicit):
     """Lane scheduling (mrp_set_schedule) only permutes which workgroup steps which lane: every
-    output and the full lane state must be bit-identical to lane-order dispatch."""
+    output and the full lane state must be bit-identical to lane-order dispatch.  Envs 1 and 5 at
+    4096 lanes (more than k_step keeps resident) run mrp_create's default, which is costliest-first
+    there (mrp_kernels.hip mrp_create), so the default path's ordering kernel over all lanes is covered."""
     from gym_puzzles_amd import Batch
-    lanes, steps = 512, 60
-    a, b = Batch(0, lanes, seed=5), Batch(0, lanes, seed=5)
-    a.set_schedule(True)
+    steps = 60
+    a, b = Batch(env_id, lanes, seed=5), Batch(env_id, lanes, seed=5)
+    if explicit:
+        a.set_schedule(True)
+    else:
+        assert a.get_schedule() == 1, "costliest-first is the default for this env above the resident lanes"
     b.set_schedule(False)
+    assert b.get_schedule() == 0
     for x in (a, b):
         x.set_auto_reset(True)
         x.set_time_limit(25)

@@ -15,7 +15,7 @@ import numpy as np
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from gym_puzzles_amd import Batch, _native  # noqa: E402
 
-TW = 24
+TW = _native.trace_words()
 vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
 
 

@@ -26,7 +26,7 @@ def main():
     for _ in range(warmup):
         b.step()
     L = _native.load()
-    tr = np.zeros((lanes, 32), np.uint32)
+    tr = np.zeros((lanes, _native.trace_words()), np.uint32)
     vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
     states, lanes_, traces, totals = [], [], [], []
     for _ in range(steps):

@@ -25,7 +25,7 @@ def main():
     repeat = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     env = int(cap["env"])
     L = _native.load()
-    tr = np.zeros((1, 32), np.uint32)
+    tr = np.zeros((1, _native.trace_words()), np.uint32)
     rows = []
     for k in range(len(cap["lane"])):
         lane = int(cap["lane"][k])

@@ -33,8 +33,8 @@ def main():
     for _ in range(warmup):
         b.step()
     L = _native.load()
-    tr = np.zeros((lanes, 32), np.uint32)
-    acc = np.zeros((lanes, 32), np.float64)
+    tr = np.zeros((lanes, _native.trace_words()), np.uint32)
+    acc = np.zeros((lanes, _native.trace_words()), np.float64)
     slow_block = np.zeros((lanes + 1023) // 1024, np.int64)
     last_block = np.zeros_like(slow_block)
     launches = []

@@ -15,15 +15,16 @@ NAMES = "load act fnc0 coll solve fnc1 toi obs out reset store".split()
 
 
 def trace(L, n):
-    tr = np.zeros((n, 32), np.uint32)
+    tr = np.zeros((n, _native.trace_words()), np.uint32)
     L.mrp_debug_trace(0, tr.ctypes.data_as(ctypes.c_void_p), n)
     return tr
 
 
 def row(r):
     return (f"{r[11]:9d} | " + " ".join(f"{v:7d}" for v in r[:11]) + f" | nc {r[12]} toi {r[13]} pos {r[14]} vel {r[15]}"
-            f" | vel {r[16]} pos {r[17]} pre {r[18]} maxisl {r[19]} "
-            + " ".join(f"{(v >> 8) & 255}-{v & 255}" for v in r[20:24] if v != 0xffffffff))
+            f" | vel {r[16]} pos {r[17]} pre {r[18]} maxisl {r[19]}"
+            # words 20-23 are cycle splits since round 4 (mrp_world.h g_trace), not body pairs
+            f" | toi scan {r[20]} events {r[21]} | collide narrow {r[22]} commit {r[23]}")
 
 
 env = int(sys.argv[1]) if len(sys.argv) > 1 else 0

@@ -43,7 +43,7 @@ def main():
     pmax, smax, rt = np.zeros(16, np.uint64), np.zeros(256, np.uint64), np.zeros(2, np.uint64)
     assert L.mrp_debug_stamps(0, vp(buf)) == 0, "not a -DMRP_STAMPS build of this env"
     L.mrp_debug_stamps_ext(0, vp(pmax), vp(smax), vp(rt))
-    tr = np.zeros((lanes, 32), np.uint32)
+    tr = np.zeros((lanes, _native.trace_words()), np.uint32)
     slow = []          # per launch: the slowest lane's trace row
     slow10 = []        # per launch: mean trace row of the 10 slowest lanes
     for _ in range(steps):
