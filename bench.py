@@ -229,6 +229,14 @@ def main():
     ap.add_argument("--lanes", type=int, default=4096, help="lanes (worlds) per GPU")
     ap.add_argument("--seed", type=int, default=17)
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the per-step gather to rank 0")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="N>1: torch.distributed backend; nccl = RCCL over xGMI (the default), gloo = the same "
+                         "code path with the packed [L, O+2] block staged through pinned host memory (runs "
+                         "with several ranks on one GPU, where RCCL refuses duplicate devices)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="N>1 rehearsal on one GPU: every rank uses device 0 (with --dist-backend gloo)")
+    ap.add_argument("--dump-gather", default="",
+                    help="N>1 check: rank 0 saves every timed step's gathered (obs | reward | done) rows to this .npy")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--schedule", type=int, default=-1, help="mrp_set_schedule mode: 0 lane order, 1 costliest-first dispatch, 2 cost priority, 3 both; default: the library's per-env choice (mrp_create)")
     ap.add_argument("--time-every", type=int, default=0,
@@ -265,13 +273,19 @@ def main():
     distributed = world > 1
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (libmrp has no CPU fallback)")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    gpu = 0 if args.same_device else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    host_coll = distributed and args.dist_backend == "gloo"
     if distributed:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if host_coll:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    cdev = torch.device("cpu") if host_coll else dev   # where the small control collectives run
 
     L = args.lanes
-    b = Batch(args.env, L, device=local_rank, seed=args.seed, lane_offset=rank * L)
+    b = Batch(args.env, L, device=gpu, seed=args.seed, lane_offset=rank * L)
     # a dedicated (non-NULL) stream shared by the library and torch, so the HIP events that
     # time k_step are recorded on the stream the kernel runs on
     stream = torch.cuda.Stream(dev)
@@ -287,7 +301,8 @@ def main():
     trunc = torch.zeros(L, dtype=torch.uint8, device=dev)
     status = torch.zeros(L, dtype=torch.uint8, device=dev)
     # one contiguous buffer per rank for the gather: [obs | reward | done] as float32
-    gather = StepGather(Shard(rank, world, L), O, dev) if distributed and not args.no_gather else None
+    gather = StepGather(Shard(rank, world, L), O, dev, host_stage=host_coll) if distributed and not args.no_gather else None
+    dumps = [] if (args.dump_gather and rank == 0 and gather is not None) else None
 
     b.reset()   # device-RNG spawns for every lane (seeded by global lane id)
     norm = None
@@ -339,6 +354,8 @@ def main():
             norm.step(obs, rew, done, nobs, nrew, term, nterm, epr, epl)
         if gather is not None:
             gather(nobs if norm is not None else obs, nrew if norm is not None else rew, done)
+            if dumps is not None:
+                dumps.append(gather.full.to("cpu", copy=True))
     r1.record(stream)
     torch.cuda.synchronize(dev)
     if distributed:
@@ -366,7 +383,7 @@ def main():
            "nonfinite_lane_steps": int(ctr_window["nonfinite_steps"])}
     if distributed:
         t = torch.tensor([elapsed, kern_ms, bad["lanes_with_loop_guard_fault"], 0 if bad["obs_finite"] else 1,
-                          bad["nonfinite_lane_steps"]], dtype=torch.float64, device=dev)
+                          bad["nonfinite_lane_steps"]], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
         bad = {"lanes_with_loop_guard_fault": int(t[2]), "obs_finite": not bool(t[3]), "nonfinite_lane_steps": int(t[4])}
@@ -467,6 +484,8 @@ def main():
             "config": {"workload": f"{ENV_NAMES[args.env]}, {L} lanes/GPU, random actions, auto-reset", "env_id": args.env,
                        "lanes_per_gpu": L, "global_lanes": world * L,
                        "parallelism": f"lane-sharded x{world}" + ("" if world == 1 or args.no_gather else " + gather to rank 0/step"),
+                       "collective": None if world == 1 else (args.dist_backend + (" (host-staged)" if host_coll else " (RCCL)")),
+                       "devices": 1 if (world == 1 or args.same_device) else world,
                        "vecnormalize": bool(args.vecnormalize),
                        "dispatch": ("lane order" if args.schedule == 0 else f"mrp_set_schedule({args.schedule})") if args.schedule >= 0
                                    else "library default (costliest-first for Heavy-v0 / v3 beyond the resident waves, else lane order)"},
@@ -494,6 +513,8 @@ def main():
             cb = line["cpu_baseline"]
             cb["gpu_over_cpu"] = {"port": value / cb["value"], "early_exit_port": value / cb["early_exit_port"]["value"]}
         print(json.dumps(line), flush=True)
+    if dumps is not None:
+        np.save(args.dump_gather, torch.stack(dumps).numpy())
     b.close()
     if distributed:
         dist.destroy_process_group()

@@ -40,15 +40,20 @@ def shard_from_env(lanes_per_rank: int) -> Shard:
 class StepGather:
     """Packs one step's outputs of this rank and gathers every rank's block to rank 0."""
 
-    def __init__(self, shard: Shard, obs_dim: int, device, group=None, to_all: bool = False):
+    def __init__(self, shard: Shard, obs_dim: int, device, group=None, to_all: bool = False, host_stage: bool = False):
+        """``host_stage``: the collective runs on host memory (a CPU backend such as gloo): the packed
+        block is copied from the device into a pinned host buffer and gathered there; the receive
+        buffer is on the host too."""
         import torch
         self.shard, self.obs_dim, self.group, self.to_all = shard, obs_dim, group, to_all
         L = shard.lanes_per_rank
         self.packed = torch.zeros((L, obs_dim + 2), dtype=torch.float32, device=device)
+        self.host = torch.zeros((L, obs_dim + 2), dtype=torch.float32).pin_memory() if host_stage else None
         root = shard.rank == 0 or to_all
         # the receive blocks are row slices of ONE [G, obs_dim + 2] buffer: the gathered step is
         # contiguous on arrival, no concatenation afterwards
-        self.full = torch.zeros((shard.global_lanes, obs_dim + 2), dtype=torch.float32, device=device) if root else None
+        rdev = "cpu" if host_stage else device
+        self.full = torch.zeros((shard.global_lanes, obs_dim + 2), dtype=torch.float32, device=rdev) if root else None
         self.blocks = list(self.full.split(L, dim=0)) if root else None
 
     def pack(self, obs, reward, done):
@@ -63,6 +68,9 @@ class StepGather:
         are views of this gatherer's receive buffer, valid until its next call."""
         import torch.distributed as dist
         p = self.pack(obs, reward, done)
+        if self.host is not None:
+            self.host.copy_(p)   # synchronous device -> pinned host copy: the CPU collective reads it next
+            p = self.host
         if self.shard.world == 1:
             full = p
         else:
