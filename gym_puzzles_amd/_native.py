@@ -49,7 +49,7 @@ EXPORTED = (
     "mrp_step_n_device", "mrp_set_auto_reset", "mrp_set_frameskip", "mrp_set_seed", "mrp_set_schedule", "mrp_get_schedule",
     "mrp_get_bodies", "mrp_get_flags", "mrp_get_faults", "mrp_counters", "mrp_counters_ex", "mrp_state_words", "mrp_get_state", "mrp_set_state",
     "mrp_set_time_limit", "mrp_selftest_sincos", "mrp_debug_stamps", "mrp_debug_stamps_ext",
-    "mrp_debug_trace", "mrp_debug_trace_words", "mrp_debug_progress", "mrp_debug_velbench", "mrp_norm_create", "mrp_norm_destroy", "mrp_norm_last_error", "mrp_norm_set_stream",
+    "mrp_debug_trace", "mrp_debug_trace_words", "mrp_debug_progress", "mrp_debug_velbench", "mrp_debug_posbench", "mrp_norm_create", "mrp_norm_destroy", "mrp_norm_last_error", "mrp_norm_set_stream",
     "mrp_norm_set_training", "mrp_norm_set_norm_obs", "mrp_norm_reset_device", "mrp_norm_step_device", "mrp_norm_step_device_ex", "mrp_norm_get_stats", "mrp_norm_set_stats",
     "mrp_render", "mrp_render_device", "mrp_get_goals", "mrp_shapes",
 )
@@ -132,6 +132,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.mrp_debug_trace_words.argtypes = []
     L.mrp_debug_progress.argtypes = [i, ctypes.POINTER(P), i]
     L.mrp_debug_velbench.argtypes = [i, i, i, i, i, P]
+    if hasattr(L, "mrp_debug_posbench"):   # A/B libraries built before round 5's position micro-benchmark lack it
+        L.mrp_debug_posbench.argtypes = [i, i, i, i, i, P]
     _lib = L
     return L
 

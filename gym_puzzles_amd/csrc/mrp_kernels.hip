@@ -583,6 +583,20 @@ int mrp_debug_velbench(int device, int nc, int pcount, int iters, int blocks, ui
     return e == hipSuccess ? MRP_OK : MRP_E_HIP;
 }
 
+int mrp_debug_posbench(int device, int nc, int pcount, int iters, int blocks, uint64_t* out) {
+    if (nc < 1 || nc > 6 || pcount < 1 || pcount > 2 || iters < 1 || blocks < 1 || !out || hipSetDevice(device) != hipSuccess)
+        return MRP_E_ARG;
+    EnvTables all[N_ENVS];
+    for (int i = 0; i < N_ENVS; ++i) build_tables(i, all[i]);
+    unsigned long long* d = nullptr;
+    if (hipMalloc((void**)&d, (size_t)blocks * 16) != hipSuccess) return MRP_E_HIP;
+    hipError_t e = posbench_launch(all, nc, pcount, iters, blocks, d);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out, d, (size_t)blocks * 16, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    return e == hipSuccess ? MRP_OK : MRP_E_HIP;
+}
+
 // Diagnostic builds only: read-and-clear one stamp symbol of every env unit, combined by sum
 // (or max); only the units whose kernels ran hold non-zero values.
 // A variant library (build.py --variant ... -DMRP_STAMPS) instruments only the env units it lists;

@@ -671,7 +671,50 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_velbench(int n
     __syncthreads();
     if (tid == 0) out[blockIdx.x] = t1 - t0 + (is.vvx[0] == 12345.0f ? 1ull : 0ull);
 }
+// Diagnostic micro-benchmark of the position passes (mrp_debug_posbench): a synthetic island of nc
+// static-wall contacts of pcount points on one moving block (body 0), walls alternately above and
+// below it, each penetrating it by ~0.1 (the squeezed shape of the slowest v0 lanes: the passes never
+// reach the exit test), solved by the dispatch of the step (register paths for 1-2 contacts, the
+// lanes path above); out[2 * block] = s_memtime cycles, out[2 * block + 1] = passes run.
+__global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_posbench(int nc, int pcount, int iters, unsigned long long* out) {
+    using W = World<0>;
+    __shared__ Shared<0> sh;
+    const int tid = threadIdx.x;
+    EnvParams P{};
+    W w(sh, g_table, P, tid);
+    auto& is = sh.isl;
+    if (tid == 0) {
+        is.nb = nc + 1; is.nc = nc;
+        is.pcx[0] = 0.0f; is.pcy[0] = 0.0f; is.pa[0] = 0.3f; is.vvx[0] = 0.0f; is.vvy[0] = 0.0f; is.vw[0] = 0.0f;
+        for (int i = 0; i < nc; ++i) {
+            const float up = (i & 1) ? -1.0f : 1.0f;   // wall above (normal down) or below (normal up)
+            is.pcx[i + 1] = 0.05f * (float)i; is.pcy[i + 1] = up; is.pa[i + 1] = 0.0f;
+            is.vvx[i + 1] = 0.0f; is.vvy[i + 1] = 0.0f; is.vw[i + 1] = 0.0f;
+            VC& vc = sh.u.sol.vcs[i];
+            PC& pc = sh.u.sol.pcs[i];
+            vc.iaI = i + 1; vc.ibI = 0; vc.mA = 0.0f; vc.iA = 0.0f; vc.mB = 0.05f; vc.iB = 1.0f / 17.0833f;
+            vc.pointCount = pcount;
+            pc.type = MT_FACEA; pc.pointCount = pcount;
+            pc.lnx = 0.0f; pc.lny = -up; pc.lpx0 = 0.0f; pc.lpy0 = -0.5f * up;
+            pc.lpx[0] = -0.2f; pc.lpy[0] = 0.62f * up; pc.lpx[1] = 0.2f; pc.lpy[1] = 0.6f * up;
+            pc.lcAx = 0.0f; pc.lcAy = 0.0f; pc.lcBx = 0.0f; pc.lcBy = 0.0f; pc.rA = 0.01f; pc.rB = 0.01f;
+        }
+    }
+    __syncthreads();
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    int n = w.solver_position_small(is, sh.u.sol.vcs, sh.u.sol.pcs, false, -1, -1, iters);
+    if (n < 0) n = w.template solver_position_lanes<false>(is, sh.u.sol.vcs, sh.u.sol.pcs, false, -1, -1, iters);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (tid == 0) { out[2 * blockIdx.x] = t1 - t0 + (is.pcx[0] == 12345.0f ? 1ull : 0ull); out[2 * blockIdx.x + 1] = (unsigned long long)n; }
+}
 }  // namespace
+hipError_t mrp::posbench_launch(const EnvTables* all, int nc, int pcount, int iters, int blocks, unsigned long long* d_out) {
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_table), all, sizeof(EnvTables));
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_posbench, dim3(blocks), dim3(BLOCK), 0, nullptr, nc, pcount, iters, d_out);
+    return hipGetLastError();
+}
 hipError_t mrp::velbench_launch(const EnvTables* all, int nc, int pcount, int iters, int blocks, unsigned long long* d_out) {
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_table), all, sizeof(EnvTables));
     if (e != hipSuccess) return e;

@@ -86,6 +86,8 @@ extern const EnvOps g_env_ops_0, g_env_ops_1, g_env_ops_2, g_env_ops_3, g_env_op
     g_env_ops_15, g_env_ops_16, g_env_ops_17, g_env_ops_18, g_env_ops_19, g_env_ops_20, g_env_ops_21, g_env_ops_22;
 // defined in mrp_env0.hip: the lane-distributed velocity-sweep micro-benchmark (mrp_debug_velbench)
 hipError_t velbench_launch(const EnvTables* all, int nc, int pcount, int iters, int blocks, unsigned long long* d_out);
+// defined in mrp_env0.hip: the position-pass micro-benchmark (mrp_debug_posbench)
+hipError_t posbench_launch(const EnvTables* all, int nc, int pcount, int iters, int blocks, unsigned long long* d_out);
 
 inline const EnvOps* env_ops(int env_id) {
     static const EnvOps* const t[N_ENVS] = {&g_env_ops_0,  &g_env_ops_1,  &g_env_ops_2,  &g_env_ops_3,  &g_env_ops_4,

@@ -60,6 +60,47 @@ constexpr int NULLN = -1;
 #ifndef MRP_LANES_PAIRS
 #define MRP_LANES_PAIRS 0
 #endif
+// Velocity-update variants (round 5 A/B; each keeps every float operation and its order):
+// MRP_VEL_PICK2  the block solver's case tests as two ballots of the compares (no bool in a VGPR)
+// MRP_VEL_NEGNM  -K^-1 stored per contact, so the case-1 impulse x needs no negation
+// MRP_VEL_VTCROSS  the tangent speed b2Dot(dv, (n.y, -n.x)) as dv.x*n.y - dv.y*n.x (pcross: a + (-b) is
+//                a - b exactly), so the tangent is never materialised for it
+// MRP_VEL_EXPECT  case 1 of the block solver (both points active) laid out as the fall-through path
+// MRP_VEL_SPLIT  case 1 applies its impulse on a path of its own (no join with the rarer cases)
+// MRP_VEL_SPEC   case 1 applied speculatively, its test resolved afterwards (restore + cases 2-4 if not)
+#ifndef MRP_VEL_PICK2
+#define MRP_VEL_PICK2 0
+#endif
+#ifndef MRP_VEL_NEGNM
+#define MRP_VEL_NEGNM 0
+#endif
+#ifndef MRP_VEL_VTCROSS
+#define MRP_VEL_VTCROSS 0
+#endif
+#ifndef MRP_VEL_EXPECT
+#define MRP_VEL_EXPECT 0
+#endif
+#ifndef MRP_VEL_SPLIT
+#define MRP_VEL_SPLIT 0
+#endif
+#ifndef MRP_VEL_SPEC
+#define MRP_VEL_SPEC 0
+#endif
+#if MRP_VEL_EXPECT
+#define MRP_UNLIKELY(c) __builtin_expect(!!(c), 0)
+#define MRP_LIKELY(c) __builtin_expect(!!(c), 1)
+#else
+#define MRP_UNLIKELY(c) (c)
+#define MRP_LIKELY(c) (c)
+#endif
+#if MRP_VEL_VTCROSS
+#define MRP_VT(dv, n, t) pcross(dv, n)
+// lambda * (n.y, -n.x) = (lambda*n.y, -(lambda*n.x)) exactly: a swapped product with its high half negated
+#define MRP_PT(l, n, t) ([](const P2 q_) { return p2(q_.x, -q_.y); }(pbc(l) * (n).yx))
+#else
+#define MRP_VT(dv, n, t) pdot(dv, t)
+#define MRP_PT(l, n, t) (pbc(l) * (t))
+#endif
 #ifdef MRP_XW_INLINE
 #define MRP_XW_FN __device__ __forceinline__
 #else
@@ -1158,7 +1199,7 @@ template <int ENV> struct World {
                 P2 vA = p2(rdl(bvx, ia[i]), rdl(bvy, ia[i])); float wA = rdl(bw, ia[i]);
                 P2 vB = p2(rdl(bvx, ib[i]), rdl(bvy, ib[i])); float wB = rdl(bw, ib[i]);
                 P2 ni, ti;
-                vel_update(my, pc[i], [i](bool x) { return lane_bit(x, i); }, ni, ti, vA, wA, vB, wB);
+                vel_update(my, pc[i], PickLane{i}, ni, ti, vA, wA, vB, wB);
                 if (tid == i) { my.ni = ni; my.ti = ti; }
                 bvx = wrl(bvx, rdl(vA.x, i), ia[i]); bvy = wrl(bvy, rdl(vA.y, i), ia[i]); bw = wrl(bw, rdl(wA, i), ia[i]);
                 bvx = wrl(bvx, rdl(vB.x, i), ib[i]); bvy = wrl(bvy, rdl(vB.y, i), ib[i]); bw = wrl(bw, rdl(wB, i), ib[i]);
@@ -1231,7 +1272,7 @@ template <int ENV> struct World {
                 P2 ni, ti;
                 // the block solver's case is decided by lane i's values (wave-uniform branches);
                 // the other lanes follow lane i's case and are discarded
-                vel_update(my, pcount, [i](bool x) { return lane_bit(x, i); }, ni, ti, vA, wA, vB, wB);
+                vel_update(my, pcount, PickLane{i}, ni, ti, vA, wA, vB, wB);
                 if (tid == i) { my.ni = ni; my.ti = ti; }
                 // lane i's results go to the lanes of bodies A and B (A first, as the reference stores)
                 bvx = wrl(bvx, rdl(vA.x, i), ia); bvy = wrl(bvy, rdl(vA.y, i), ia); bw = wrl(bw, rdl(wA, i), ia);
@@ -1262,6 +1303,31 @@ template <int ENV> struct World {
     // wave-uniform branches (ballot of identical lanes).  Same float operations in the same order
     // as solver_velocity, same exact early exit as solver_velocity_lanes.
     __device__ __forceinline__ static bool uni(bool c) { return __builtin_amdgcn_ballot_w64(c) != 0; }
+    // The block solver's case tests `a && b` as the wave-uniform decision.  PickUni: identical lanes
+    // (register paths); PickLane: lane i's values (lanes path).  `both` takes the two compares apart,
+    // so each ballot is the v_cmp's own lane mask (no bool materialised in a VGPR and compared back)
+    // and lane i's bit is one scalar bit test.
+    struct PickUni {
+        __device__ __forceinline__ bool operator()(bool c) const { return uni(c); }
+        __device__ __forceinline__ bool both(bool a, bool b) const {
+#if MRP_VEL_PICK2
+            return (__builtin_amdgcn_ballot_w64(a) & __builtin_amdgcn_ballot_w64(b)) != 0ull;
+#else
+            return uni(a && b);
+#endif
+        }
+    };
+    struct PickLane {
+        int i;
+        __device__ __forceinline__ bool operator()(bool c) const { return lane_bit(c, i); }
+        __device__ __forceinline__ bool both(bool a, bool b) const {
+#if MRP_VEL_PICK2
+            return ((__builtin_amdgcn_ballot_w64(a) & __builtin_amdgcn_ballot_w64(b)) >> i) & 1ull;
+#else
+            return lane_bit(a && b, i);
+#endif
+        }
+    };
     // One contact's velocity-constraint constants (VC) in registers, as packed pairs (P2: one
     // v_pk_* instruction for both halves of a b2Vec2 operation) and the impulses (the state).
     struct CC {
@@ -1280,7 +1346,12 @@ template <int ENV> struct World {
         o.rA0 = p2(-c.rAy[0], c.rAx[0]); o.rB0 = p2(-c.rBy[0], c.rBx[0]);
         o.rA1 = p2(-c.rAy[1], c.rAx[1]); o.rB1 = p2(-c.rBy[1], c.rBx[1]);
         o.normal = p2(c.nx, c.ny);
-        o.k01 = p2(c.k0, c.k1); o.k13 = p2(c.k1, c.k3); o.nm01 = p2(c.nm0, c.nm1); o.nm13 = p2(c.nm1, c.nm3);
+        o.k01 = p2(c.k0, c.k1); o.k13 = p2(c.k1, c.k3); 
+#if MRP_VEL_NEGNM
+        o.nm01 = p2(-c.nm0, -c.nm1); o.nm13 = p2(-c.nm1, -c.nm3);   // -K^-1 (see vel_update_m)
+#else
+        o.nm01 = p2(c.nm0, c.nm1); o.nm13 = p2(c.nm1, c.nm3);
+#endif
         o.nmass0 = c.nmass[0]; o.nmass1 = c.nmass[1]; o.tmass0 = c.tmass[0]; o.tmass1 = c.tmass[1];
         o.mA = pbc(c.mA); o.iA = c.iA; o.mB = pbc(c.mB); o.iB = c.iB; o.friction = c.friction;
         o.pcount = c.pointCount;
@@ -1320,13 +1391,13 @@ template <int ENV> struct World {
         ni = c.ni; ti = c.ti;
         {   // friction, point 0
             const P2 dv = ((vB + (pbc(wB) * c.rB0)) - vA) - (pbc(wA) * c.rA0);
-            const float vt = pdot(dv, tangent);
+            const float vt = MRP_VT(dv, normal, tangent);
             float lambda = c.tmass0 * (-vt);
             const float maxFriction = c.friction * ni.x;
             const float newImpulse = fclamp(ti.x + lambda, -maxFriction, maxFriction);
             lambda = newImpulse - ti.x;
             ti.x = newImpulse;
-            const P2 P = pbc(lambda) * tangent;
+            const P2 P = MRP_PT(lambda, normal, tangent);
             vA = vA - mA * P;
             wA -= iA * pcrossp(c.rA0, P);
             vB = vB + mB * P;
@@ -1334,13 +1405,13 @@ template <int ENV> struct World {
         }
         if (pcount == 2) {   // friction, point 1
             const P2 dv = ((vB + (pbc(wB) * c.rB1)) - vA) - (pbc(wA) * c.rA1);
-            const float vt = pdot(dv, tangent);
+            const float vt = MRP_VT(dv, normal, tangent);
             float lambda = c.tmass1 * (-vt);
             const float maxFriction = c.friction * ni.y;
             const float newImpulse = fclamp(ti.y + lambda, -maxFriction, maxFriction);
             lambda = newImpulse - ti.y;
             ti.y = newImpulse;
-            const P2 P = pbc(lambda) * tangent;
+            const P2 P = MRP_PT(lambda, normal, tangent);
             vA = vA - mA * P;
             wA -= iA * pcrossp(c.rA1, P);
             vB = vB + mB * P;
@@ -1367,31 +1438,78 @@ template <int ENV> struct World {
             P2 b = p2(vn1, vn2);
             b = b - (c.k01 * pbc(a.x) + c.k13 * pbc(a.y));
             // x = -(nm0*b.x + nm2*b.y, nm1*b.x + nm3*b.y), nm2 = nm1
+#if MRP_VEL_NEGNM
+            // c.nm01 / c.nm13 hold -K^-1: (-nm0)*b.x + (-nm1)*b.y = -(nm0*b.x + nm1*b.y) exactly (negation
+            // commutes with round-to-nearest), so the case-1 impulse needs no negation of its own
+            P2 x = c.nm01 * pbc(b.x) + c.nm13 * pbc(b.y);
+#else
             P2 x = -(c.nm01 * pbc(b.x) + c.nm13 * pbc(b.y));
-            bool ok = true;
-            if (!pick(x.x >= 0.0f && x.y >= 0.0f)) {
-                x.x = -c.nmass0 * b.x; x.y = 0.0f;
-                vn2 = c.k01.y * x.x + b.y;
-                if (!pick(x.x >= 0.0f && vn2 >= 0.0f)) {
-                    x.x = 0.0f; x.y = -c.nmass1 * b.y;
-                    vn1 = c.k01.y * x.y + b.x;
-                    if (!pick(x.y >= 0.0f && vn1 >= 0.0f)) {
-                        x.x = 0.0f; x.y = 0.0f;
-                        ok = pick(b.x >= 0.0f && b.y >= 0.0f);
-                    }
-                }
-            }
-            if (ok) {
-                const P2 d = x - a;
+#endif
+            // Box2D's block solver applies the impulse of the first case that holds (both points
+            // active, point 1 only, point 2 only, none), or none at all
+            auto apply = [&](const P2 xs) {
+                const P2 d = xs - a;
                 const P2 P1 = pbc(d.x) * normal, P2v = pbc(d.y) * normal;
                 const P2 S = P1 + P2v;
                 vA = vA - mA * S;
                 wA -= iA * (pcrossp(c.rA0, P1) + pcrossp(c.rA1, P2v));
                 vB = vB + mB * S;
                 wB += iB * (pcrossp(c.rB0, P1) + pcrossp(c.rB1, P2v));
-                ni = x;
+                ni = xs;
+            };
+#if MRP_VEL_SPEC
+            // case 1 (both points active) applied speculatively, its test resolved after the
+            // application: the branch leaves the dependency chain.  When case 1 does not hold, the
+            // velocities and impulses are restored and cases 2-4 run as the reference orders them
+            // (same operations on the same inputs, so the same bits).
+            const P2 vA0 = vA, vB0 = vB;
+            const float wA0 = wA, wB0 = wB;
+            const bool c1 = pick.both(x.x >= 0.0f, x.y >= 0.0f);
+            apply(x);
+            asm volatile("" :: "v"(vA), "v"(vB), "v"(wA), "v"(wB), "v"(ni));   // computed before the test: no sinking
+            if (MRP_UNLIKELY(!c1)) {
+                vA = vA0; vB = vB0; wA = wA0; wB = wB0; ni = a;
+                vel_block_rare(c, pick, b, vn1, vn2, apply);
             }
+#elif MRP_VEL_SPLIT
+            // case 1 (both points active) is the straight path; the other cases branch off it and
+            // carry their own copy of the impulse application, so the common path has no join
+            if (MRP_LIKELY(pick.both(x.x >= 0.0f, x.y >= 0.0f))) {
+                apply(x);
+            } else {
+                vel_block_rare(c, pick, b, vn1, vn2, apply);
+            }
+#else
+            bool ok = true;
+            if (MRP_UNLIKELY(!pick.both(x.x >= 0.0f, x.y >= 0.0f))) {
+                x.x = -c.nmass0 * b.x; x.y = 0.0f;
+                vn2 = c.k01.y * x.x + b.y;
+                if (!pick.both(x.x >= 0.0f, vn2 >= 0.0f)) {
+                    x.x = 0.0f; x.y = -c.nmass1 * b.y;
+                    vn1 = c.k01.y * x.y + b.x;
+                    if (!pick.both(x.y >= 0.0f, vn1 >= 0.0f)) {
+                        x.x = 0.0f; x.y = 0.0f;
+                        ok = pick.both(b.x >= 0.0f, b.y >= 0.0f);
+                    }
+                }
+            }
+            if (ok) apply(x);
+#endif
         }
+    }
+    // cases 2-4 of the block solver (b2ContactSolver::SolveVelocityConstraints), each with its own
+    // application of the impulse (MRP_VEL_SPLIT)
+    template <class Pick, class Apply>
+    __device__ __forceinline__ static void vel_block_rare(const CC& c, Pick pick, const P2 b, float vn1, float vn2, Apply apply) {
+        P2 x;
+        x.x = -c.nmass0 * b.x; x.y = 0.0f;
+        vn2 = c.k01.y * x.x + b.y;
+        if (pick.both(x.x >= 0.0f, vn2 >= 0.0f)) { apply(x); return; }
+        x.x = 0.0f; x.y = -c.nmass1 * b.y;
+        vn1 = c.k01.y * x.y + b.x;
+        if (pick.both(x.y >= 0.0f, vn1 >= 0.0f)) { apply(x); return; }
+        x.x = 0.0f; x.y = 0.0f;
+        if (pick.both(b.x >= 0.0f, b.y >= 0.0f)) apply(x);
     }
     // the register-resident form: identical lanes, every lane keeps the result
     template <int PC>
@@ -1401,7 +1519,7 @@ template <int ENV> struct World {
         // of the sweep loop into registers of their own
         asm volatile("" : "+v"(c.normal));
         P2 ni, ti;
-        vel_update_t<PC>(c, [](bool x) { return uni(x); }, ni, ti, vA, wA, vB, wB);
+        vel_update_t<PC>(c, PickUni{}, ni, ti, vA, wA, vB, wB);
         c.ni = ni; c.ti = ti;
     }
     // exact early exit (see solver_velocity_lanes): the state after sweep k is compared with the
@@ -1585,7 +1703,7 @@ template <int ENV> struct World {
                                                      const float iY, P2& vX, float& wX, P2& vY, float& wY) {
         asm volatile("" : "+v"(c.normal));   // as cc_update: the tangent formed inside the packed instructions
         P2 ni, ti;
-        auto pick = [](bool x) { return uni(x); };
+        PickUni pick;
         if (wall) {
             P2 vW = p2(0.0f, 0.0f);
             float wW = 0.0f;

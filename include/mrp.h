@@ -214,6 +214,10 @@ int mrp_debug_progress(int device, uint32_t** host_words, int n_lanes);
  * contacts of pcount points) `iters` times with the early exit off; cycles[block] = s_memtime
  * cycles of the sweeps (per-contact-update cost = cycles / (iters * nc)). */
 int mrp_debug_velbench(int device, int nc, int pcount, int iters, int blocks, uint64_t* cycles);
+/* Diagnostic micro-benchmark: `blocks` workgroups each run the position passes (up to `iters`) of a
+ * synthetic island of nc static-wall contacts of pcount points squeezing one block (the passes never
+ * reach the exit test); out[2 * block] = s_memtime cycles, out[2 * block + 1] = passes run. */
+int mrp_debug_posbench(int device, int nc, int pcount, int iters, int blocks, uint64_t* out);
 
 /* ------------------------------------------------------------------------------------------
  * On-device VecNormalize + Monitor statistics.  Replaces the host-side
