@@ -62,17 +62,23 @@ constexpr int NULLN = -1;
 #endif
 // Velocity-update variants (round 5 A/B; each keeps every float operation and its order):
 // MRP_VEL_PICK2  the block solver's case tests as two ballots of the compares (no bool in a VGPR)
-// MRP_VEL_NEGNM  -K^-1 stored per contact, so the case-1 impulse x needs no negation
 // MRP_VEL_VTCROSS  the tangent speed b2Dot(dv, (n.y, -n.x)) as dv.x*n.y - dv.y*n.x (pcross: a + (-b) is
 //                a - b exactly), so the tangent is never materialised for it
 // MRP_VEL_EXPECT  case 1 of the block solver (both points active) laid out as the fall-through path
 // MRP_VEL_SPLIT  case 1 applies its impulse on a path of its own (no join with the rarer cases)
 // MRP_VEL_SPEC   case 1 applied speculatively, its test resolved afterwards (restore + cases 2-4 if not)
+// MRP_VEL_BFREE  the four cases evaluated together and picked by selects (no chain of case tests)
+#ifndef MRP_XW_LATE
+#define MRP_XW_LATE 0
+#endif
+#ifndef MRP_XW_LATE_POS
+#define MRP_XW_LATE_POS 0
+#endif
+#ifndef MRP_XW_PAIRS
+#define MRP_XW_PAIRS 0
+#endif
 #ifndef MRP_VEL_PICK2
 #define MRP_VEL_PICK2 0
-#endif
-#ifndef MRP_VEL_NEGNM
-#define MRP_VEL_NEGNM 0
 #endif
 #ifndef MRP_VEL_VTCROSS
 #define MRP_VEL_VTCROSS 0
@@ -85,6 +91,9 @@ constexpr int NULLN = -1;
 #endif
 #ifndef MRP_VEL_SPEC
 #define MRP_VEL_SPEC 0
+#endif
+#ifndef MRP_VEL_BFREE
+#define MRP_VEL_BFREE 0
 #endif
 #if MRP_VEL_EXPECT
 #define MRP_UNLIKELY(c) __builtin_expect(!!(c), 0)
@@ -1184,7 +1193,7 @@ template <int ENV> struct World {
     // readlanes take a lane select written long before (no wait states); same operations and order as
     // the generic loop below
     template <int NC>
-    MRP_LANES_FN int lanes_sweeps(Isl& is, VC* vcs, int iters, bool early_exit) {
+    MRP_LANES_FN int lanes_sweeps(Isl& is, VC* vcs, int iters, bool early_exit, int stop = 1 << 30, bool* exited = nullptr) {
         const int me = tid < NC ? tid : 0;
         CC my = load_cc(vcs[me]);
         const int cia = vcs[me].iaI, cib = vcs[me].ibI;
@@ -1213,7 +1222,9 @@ template <int ENV> struct World {
         P2 sni = my.ni, sti = my.ti;
         float sbx = bvx, sby = bvy, sbw = bw;
         bool have = ((iters - sweeps) & 3) == 2;   // the start is a snapshot point
-        while (sweeps < iters) {
+        const int last = stop < iters ? stop : iters;
+        bool ex = false;
+        while (sweeps < last) {
             sweep();
             if (STEP == 2) sweep();
             sweeps += STEP;
@@ -1223,7 +1234,7 @@ template <int ENV> struct World {
                                    (__float_as_uint(my.ti.x) ^ __float_as_uint(sti.x)) | (__float_as_uint(my.ti.y) ^ __float_as_uint(sti.y)) |
                                    (__float_as_uint(bvx) ^ __float_as_uint(sbx)) | (__float_as_uint(bvy) ^ __float_as_uint(sby)) |
                                    (__float_as_uint(bw) ^ __float_as_uint(sbw));
-                if (__builtin_amdgcn_ballot_w64(d != 0u) == 0) break;
+                if (__builtin_amdgcn_ballot_w64(d != 0u) == 0) { ex = true; break; }
             }
             if (early_exit && (left & m) == 2) {
                 sni = my.ni; sti = my.ti; sbx = bvx; sby = bvy; sbw = bw;
@@ -1232,10 +1243,27 @@ template <int ENV> struct World {
         }
         if (tid < is.nb) { is.vvx[tid] = bvx; is.vvy[tid] = bvy; is.vw[tid] = bw; }
         if (tid < NC) store_cc(vcs[tid], my);
+        if (exited) *exited = ex || sweeps >= iters;
         return sweeps;
     }
     template <int NC>
-    MRP_MAIN_FN int lanes_sweeps_main(Isl& is, VC* vcs, int iters, bool early_exit) { return lanes_sweeps<NC>(is, vcs, iters, early_exit); }
+    MRP_MAIN_FN int lanes_sweeps_main(Isl& is, VC* vcs, int iters, bool early_exit) {
+#if MRP_XW_LATE
+        // islands that have not repeated by sweep MRP_XW_LATE (the launches' slowest lanes: all 180
+        // sweeps) continue on the two-body register path when their shape has one; the others never
+        // pay its call (k_step's live registers saved around it), so short solves stay on the lanes path
+        if constexpr (XW_LATE_OK) {
+            const XwShape q = xw_shape(is, vcs);
+            if (xw_supported(q.key)) {
+                bool done = false;
+                const int k = lanes_sweeps<NC>(is, vcs, iters, early_exit, MRP_XW_LATE, &done);
+                if (done) return k;
+                return solver_velocity_xw_from(is, vcs, iters, early_exit, q, k);
+            }
+        }
+#endif
+        return lanes_sweeps<NC>(is, vcs, iters, early_exit);
+    }
     // MAIN: the call of the main island solve (b2Island::Solve), not a TOI sub-step's
     template <bool MAIN = false>
     __device__ __forceinline__ int solver_velocity_lanes(Isl& is, VC* vcs, int iters, bool early_exit = true) {
@@ -1309,6 +1337,7 @@ template <int ENV> struct World {
     // and lane i's bit is one scalar bit test.
     struct PickUni {
         __device__ __forceinline__ bool operator()(bool c) const { return uni(c); }
+        __device__ __forceinline__ bool mask(uint64_t m) const { return m != 0ull; }   // m: a ballot
         __device__ __forceinline__ bool both(bool a, bool b) const {
 #if MRP_VEL_PICK2
             return (__builtin_amdgcn_ballot_w64(a) & __builtin_amdgcn_ballot_w64(b)) != 0ull;
@@ -1320,6 +1349,7 @@ template <int ENV> struct World {
     struct PickLane {
         int i;
         __device__ __forceinline__ bool operator()(bool c) const { return lane_bit(c, i); }
+        __device__ __forceinline__ bool mask(uint64_t m) const { return (m >> i) & 1ull; }
         __device__ __forceinline__ bool both(bool a, bool b) const {
 #if MRP_VEL_PICK2
             return ((__builtin_amdgcn_ballot_w64(a) & __builtin_amdgcn_ballot_w64(b)) >> i) & 1ull;
@@ -1346,12 +1376,7 @@ template <int ENV> struct World {
         o.rA0 = p2(-c.rAy[0], c.rAx[0]); o.rB0 = p2(-c.rBy[0], c.rBx[0]);
         o.rA1 = p2(-c.rAy[1], c.rAx[1]); o.rB1 = p2(-c.rBy[1], c.rBx[1]);
         o.normal = p2(c.nx, c.ny);
-        o.k01 = p2(c.k0, c.k1); o.k13 = p2(c.k1, c.k3); 
-#if MRP_VEL_NEGNM
-        o.nm01 = p2(-c.nm0, -c.nm1); o.nm13 = p2(-c.nm1, -c.nm3);   // -K^-1 (see vel_update_m)
-#else
-        o.nm01 = p2(c.nm0, c.nm1); o.nm13 = p2(c.nm1, c.nm3);
-#endif
+        o.k01 = p2(c.k0, c.k1); o.k13 = p2(c.k1, c.k3);  o.nm01 = p2(c.nm0, c.nm1); o.nm13 = p2(c.nm1, c.nm3);
         o.nmass0 = c.nmass[0]; o.nmass1 = c.nmass[1]; o.tmass0 = c.tmass[0]; o.tmass1 = c.tmass[1];
         o.mA = pbc(c.mA); o.iA = c.iA; o.mB = pbc(c.mB); o.iB = c.iB; o.friction = c.friction;
         o.pcount = c.pointCount;
@@ -1438,13 +1463,9 @@ template <int ENV> struct World {
             P2 b = p2(vn1, vn2);
             b = b - (c.k01 * pbc(a.x) + c.k13 * pbc(a.y));
             // x = -(nm0*b.x + nm2*b.y, nm1*b.x + nm3*b.y), nm2 = nm1
-#if MRP_VEL_NEGNM
-            // c.nm01 / c.nm13 hold -K^-1: (-nm0)*b.x + (-nm1)*b.y = -(nm0*b.x + nm1*b.y) exactly (negation
-            // commutes with round-to-nearest), so the case-1 impulse needs no negation of its own
-            P2 x = c.nm01 * pbc(b.x) + c.nm13 * pbc(b.y);
-#else
+            // (not (-nm0)*b.x + (-nm1)*b.y: an exact cancellation gives +0 there where -(...) gives -0, and
+            // the stored impulse would differ in its sign bit; measured, round 5)
             P2 x = -(c.nm01 * pbc(b.x) + c.nm13 * pbc(b.y));
-#endif
             // Box2D's block solver applies the impulse of the first case that holds (both points
             // active, point 1 only, point 2 only, none), or none at all
             auto apply = [&](const P2 xs) {
@@ -1457,7 +1478,25 @@ template <int ENV> struct World {
                 wB += iB * (pcrossp(c.rB0, P1) + pcrossp(c.rB1, P2v));
                 ni = xs;
             };
-#if MRP_VEL_SPEC
+#if MRP_VEL_BFREE
+            // All four cases evaluated at once and the first that holds picked by selects, in Box2D's
+            // order (both points active; point 1 only; point 2 only; none), so no case test waits on
+            // the one before it.  The launches' slowest lanes mostly run the later cases (v0: 72 %
+            // of their 2-point updates, v2: all; oracle b2o_lcp_cases on the captured lane-steps),
+            // which the case-by-case branches reach only after one to three failed tests.
+            const float x2 = -c.nmass0 * b.x, v2 = c.k01.y * x2 + b.y;   // case 2: x = (x2, 0), vn2 = k1 x2 + b.y
+            const float x3 = -c.nmass1 * b.y, v3 = c.k01.y * x3 + b.x;   // case 3: x = (0, x3), vn1 = k1 x3 + b.x
+            const bool c1 = x.x >= 0.0f && x.y >= 0.0f, c2 = x2 >= 0.0f && v2 >= 0.0f, c3 = x3 >= 0.0f && v3 >= 0.0f;
+            P2 xs;
+            xs.x = c1 ? x.x : (c2 ? x2 : 0.0f);
+            xs.y = c1 ? x.y : (c2 ? 0.0f : (c3 ? x3 : 0.0f));
+            // some case holds (else Box2D gives up and leaves the contact unchanged): one ballot per compare
+            const uint64_t ok = (__builtin_amdgcn_ballot_w64(x.x >= 0.0f) & __builtin_amdgcn_ballot_w64(x.y >= 0.0f)) |
+                                (__builtin_amdgcn_ballot_w64(x2 >= 0.0f) & __builtin_amdgcn_ballot_w64(v2 >= 0.0f)) |
+                                (__builtin_amdgcn_ballot_w64(x3 >= 0.0f) & __builtin_amdgcn_ballot_w64(v3 >= 0.0f)) |
+                                (__builtin_amdgcn_ballot_w64(b.x >= 0.0f) & __builtin_amdgcn_ballot_w64(b.y >= 0.0f));
+            if (pick.mask(ok)) apply(xs);
+#elif MRP_VEL_SPEC
             // case 1 (both points active) applied speculatively, its test resolved after the
             // application: the branch leaves the dependency chain.  When case 1 does not hold, the
             // velocities and impulses are restored and cases 2-4 run as the reference orders them
@@ -1574,13 +1613,15 @@ template <int ENV> struct World {
     // the NS values of the sweep state.  Every compare point has iters - k even, so the sweeps run in
     // pairs and the loop carries no per-sweep parity test or exit bookkeeping (an odd count runs its
     // first sweep alone); returns the sweeps run.
+    // `start` > 0: continuing after `start` sweeps of another path whose last compare point was sweep
+    // `start` (MRP_XW_LATE; even, as every compare point is): no snapshot is held yet
     template <int NS, class Sweep, class State>
-    __device__ __forceinline__ static int sweep_pairs(int iters, bool early_exit, Sweep sweep, State state) {
-        int it = 0;
-        if (iters & 1) { sweep(); it = 1; }
+    __device__ __forceinline__ static int sweep_pairs(int iters, bool early_exit, Sweep sweep, State state, int start = 0) {
+        int it = start;
+        if ((iters - start) & 1) { sweep(); it += 1; }
         float cur[NS];
         state(cur);
-        Snap<NS> snap(cur, ((iters - it) & 3) == 2);
+        Snap<NS> snap(cur, start == 0 && ((iters - it) & 3) == 2);
         while (it < iters) {
             sweep();
             sweep();
@@ -1699,6 +1740,10 @@ template <int ENV> struct World {
     // -6 % over a whole episode (the call and its register saves per island solve); off by default
     static constexpr bool XW_PATHS = false;
 #endif
+    // MRP_XW_LATE=N (sweeps) / MRP_XW_LATE_POS=N (passes): the main island solve's 3-4 contact islands
+    // of a two-body shape run the lanes path for N sweeps (passes) and, when they have not exited by then,
+    // the two-body register path for the rest (the call is paid only by the long solves)
+    static constexpr bool XW_LATE_OK = ENV == 0 && (MRP_XW_LATE > 0 || MRP_XW_LATE_POS > 0);
     __device__ __forceinline__ static void xw_update(CC& c, bool wall, bool two, const P2 mX, const float iX, const P2 mY,
                                                      const float iY, P2& vX, float& wX, P2& vY, float& wY) {
         asm volatile("" : "+v"(c.normal));   // as cc_update: the tangent formed inside the packed instructions
@@ -1721,7 +1766,7 @@ template <int ENV> struct World {
         return -1;
     }
     template <int NC, int MASK>
-    MRP_XW_FN int sweep_xw(Isl& is, VC* vcs, int iters, bool early_exit, int x, int y, int pcm) {
+    MRP_XW_FN int sweep_xw(Isl& is, VC* vcs, int iters, bool early_exit, int x, int y, int pcm, int start = 0) {
         constexpr int FY = xw_first_y<MASK, NC>();
         constexpr int NS = 6 + 4 * NC;
         CC c[NC];
@@ -1739,11 +1784,21 @@ template <int ENV> struct World {
 #pragma unroll
             for (int i = 0; i < NC; ++i) { v[6 + 4 * i] = c[i].ni.x; v[7 + 4 * i] = c[i].ni.y; v[8 + 4 * i] = c[i].ti.x; v[9 + 4 * i] = c[i].ti.y; }
         };
+#if MRP_XW_PAIRS
+        // two sweeps per loop trip, the exit bookkeeping once per pair (as the one- and two-contact
+        // register paths: sweep_pairs)
+        const int sweeps = sweep_pairs<NS>(iters, early_exit, [&] {
+#pragma unroll
+            for (int i = 0; i < NC; ++i) xw_update(c[i], (MASK >> i) & 1, (pcm >> i) & 1, mX, iX, mY, iY, vX, wX, vY, wY);
+        }, state, start);
+#else
         float init[NS];
         state(init);
-        Snap<NS> snap(init, snap_initial(iters));
-        int sweeps = 0;
-        for (int it = 0; it < iters; ++it) {
+        // start > 0: continuing the lanes path's sweeps (MRP_XW_LATE); its last compare point was
+        // sweep `start`, so no snapshot is held and the schedule resumes at the next snapshot point
+        Snap<NS> snap(init, start == 0 ? snap_initial(iters) : false);
+        int sweeps = start;
+        for (int it = start; it < iters; ++it) {
             ++sweeps;
 #pragma unroll
             for (int i = 0; i < NC; ++i) xw_update(c[i], (MASK >> i) & 1, (pcm >> i) & 1, mX, iX, mY, iY, vX, wX, vY, wY);
@@ -1753,6 +1808,7 @@ template <int ENV> struct World {
                 if (snap.step(it, iters, cur)) break;
             }
         }
+#endif
         if (tid == 0) {
             is.vvx[x] = vX.x; is.vvy[x] = vX.y; is.vw[x] = wX;
             if (FY >= 0) { is.vvx[y] = vY.x; is.vvy[y] = vY.y; is.vw[y] = wY; }
@@ -1787,6 +1843,19 @@ template <int ENV> struct World {
     }
     // the shapes instantiated (the v0 driver window's 3-4 contact islands, by velocity updates: (3, 4)
     // 24 %, (3, 7) 14 %, (4, 15) 13 %, (3, 6) 9 %, (4, 12) 8 %; oracle b2o_topo_diag, round 4)
+    __device__ __forceinline__ static bool xw_supported(int key) {
+        return key == 3 * 16 + 4 || key == 3 * 16 + 6 || key == 3 * 16 + 7 || key == 4 * 16 + 12 || key == 4 * 16 + 15;
+    }
+    // the same shapes, continuing after `start` sweeps of the lanes path (MRP_XW_LATE)
+    __device__ __forceinline__ int solver_velocity_xw_from(Isl& is, VC* vcs, int iters, bool early_exit, const XwShape q, int start) {
+        switch (q.key) {
+            case 3 * 16 + 4: return sweep_xw<3, 4>(is, vcs, iters, early_exit, q.x, q.y, q.pcm, start);
+            case 3 * 16 + 6: return sweep_xw<3, 6>(is, vcs, iters, early_exit, q.x, q.y, q.pcm, start);
+            case 3 * 16 + 7: return sweep_xw<3, 7>(is, vcs, iters, early_exit, q.x, q.y, q.pcm, start);
+            case 4 * 16 + 12: return sweep_xw<4, 12>(is, vcs, iters, early_exit, q.x, q.y, q.pcm, start);
+            default: return sweep_xw<4, 15>(is, vcs, iters, early_exit, q.x, q.y, q.pcm, start);
+        }
+    }
     __device__ __forceinline__ int solver_velocity_xw(Isl& is, VC* vcs, int iters, bool early_exit = true) {
         if constexpr (!XW_PATHS) return -1;
         const XwShape q = xw_shape(is, vcs);
@@ -1984,7 +2053,7 @@ template <int ENV> struct World {
     // unchanged by a finite impulse (c + 0 * P = c, a + 0 * x = a), so it is not written back.  Same
     // float operations in the same order as solver_position; one wave-uniform rotation memo.
     template <int NC, int MASK>
-    MRP_XW_FN int pos_xw(Isl& is, const VC* vcs, const PC* pcs, int iters, int x, int y) {
+    MRP_XW_FN int pos_xw(Isl& is, const VC* vcs, const PC* pcs, int iters, int x, int y, int start = 0) {
         constexpr int FY = xw_first_y<MASK, NC>();
         PCC c[NC];
         P2 cW[NC];
@@ -2007,7 +2076,7 @@ template <int ENV> struct World {
         if (FY >= 0) { cY = p2(is.pcx[y], is.pcy[y]); aY = is.pa[y]; }
         UniMemo memo;
         auto get = [&memo](float a) { return memo.get(a); };
-        int it = 0;
+        int it = start;   // passes already run by the lanes path (MRP_XW_LATE_POS)
         while (it < iters) {
             ++it;
             float minSep = 0.0f;
@@ -2030,6 +2099,15 @@ template <int ENV> struct World {
         }
         return it;
     }
+    __device__ __forceinline__ int solver_position_xw_from(Isl& is, const VC* vcs, const PC* pcs, int iters, const XwShape q, int start) {
+        switch (q.key) {
+            case 3 * 16 + 4: return pos_xw<3, 4>(is, vcs, pcs, iters, q.x, q.y, start);
+            case 3 * 16 + 6: return pos_xw<3, 6>(is, vcs, pcs, iters, q.x, q.y, start);
+            case 3 * 16 + 7: return pos_xw<3, 7>(is, vcs, pcs, iters, q.x, q.y, start);
+            case 4 * 16 + 12: return pos_xw<4, 12>(is, vcs, pcs, iters, q.x, q.y, start);
+            default: return pos_xw<4, 15>(is, vcs, pcs, iters, q.x, q.y, start);
+        }
+    }
     __device__ __forceinline__ int solver_position_xw(Isl& is, const VC* vcs, const PC* pcs, int iters) {
         if constexpr (!XW_PATHS) return -1;
         const XwShape q = xw_shape(is, vcs);
@@ -2046,7 +2124,8 @@ template <int ENV> struct World {
     // position passes of islands of NC = 3 or 4 contacts with the schedule (bodies, point counts,
     // manifold types) read out of the lanes once, before the passes (see lanes_sweeps)
     template <int NC>
-    MRP_LANES_FN int lanes_passes(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB, int iters) {
+    MRP_LANES_FN int lanes_passes(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB, int iters,
+                                  int stop = 1 << 30, bool* exited = nullptr) {
         const int me = tid < NC ? tid : 0;
         const PCC my = load_pcc(vcs[me], pcs[me], toi, toiA, toiB);
         const int cia = vcs[me].iaI, cib = vcs[me].ibI;
@@ -2059,7 +2138,9 @@ template <int ENV> struct World {
         for (int i = 0; i < NC; ++i) { ia[i] = rdli(cia, i); ib[i] = rdli(cib, i); pc[i] = rdli(my.pcount, i); ty[i] = rdli(my.type, i); }
         RotMemo memo;
         int it = 0;
-        while (it < iters) {
+        const int last = stop < iters ? stop : iters;
+        bool ex = false;
+        while (it < last) {
             ++it;
             float minSep = 0.0f;
 #pragma unroll
@@ -2072,13 +2153,25 @@ template <int ENV> struct World {
                 bx = wrl(bx, rdl(cA.x, i), ia[i]); by = wrl(by, rdl(cA.y, i), ia[i]); ba = wrl(ba, rdl(aA, i), ia[i]);
                 bx = wrl(bx, rdl(cB.x, i), ib[i]); by = wrl(by, rdl(cB.y, i), ib[i]); ba = wrl(ba, rdl(aB, i), ib[i]);
             }
-            if (minSep >= exitSep) break;
+            if (minSep >= exitSep) { ex = true; break; }
         }
         if (tid < is.nb) { is.pcx[tid] = bx; is.pcy[tid] = by; is.pa[tid] = ba; }
+        if (exited) *exited = ex || it >= iters;
         return it;
     }
     template <int NC>
     MRP_MAIN_FN int lanes_passes_main(Isl& is, const VC* vcs, const PC* pcs, int iters) {
+#if MRP_XW_LATE_POS
+        if constexpr (XW_LATE_OK) {   // see lanes_sweeps_main
+            const XwShape q = xw_shape(is, vcs);
+            if (xw_supported(q.key)) {
+                bool done = false;
+                const int k = lanes_passes<NC>(is, vcs, pcs, false, -1, -1, iters, MRP_XW_LATE_POS, &done);
+                if (done) return k;
+                return solver_position_xw_from(is, vcs, pcs, iters, q, k);
+            }
+        }
+#endif
         return lanes_passes<NC>(is, vcs, pcs, false, -1, -1, iters);
     }
     template <bool MAIN = false>

@@ -21,6 +21,7 @@
 
 #include <float.h>
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -1049,6 +1050,18 @@ static inline V2 mat_mul(const float* M, V2 v) {   /* M = {ex.x, ex.y, ey.x, ey.
     return v2(M[0] * v.x + M[2] * v.y, M[1] * v.x + M[3] * v.y);
 }
 
+/* diagnostic (b2o_lcp_cases): how often each case of the 2-point block solver applies (cases 1-4,
+ * then "no solution"), counted over every 2-point velocity update since the last reset; plus the
+ * 1-point updates and the updates whose normal impulses are subnormal (tools: chain analysis) */
+#ifndef OR_NO_WORK
+static long g_lcp[8];
+#define LCP_CASE(k) do { _Pragma("omp atomic") g_lcp[k]++; } while (0)
+void b2o_lcp_cases(long* out8, int reset) {
+    for (int k = 0; k < 8; ++k) { if (out8) out8[k] = g_lcp[k]; if (reset) g_lcp[k] = 0; }
+}
+#else
+#define LCP_CASE(k) do {} while (0)
+#endif
 static void solver_solve_velocity(Solver* s) {
     for (int i = 0; i < s->count; ++i) {
         VC* vc = s->vcs + i;
@@ -1097,15 +1110,16 @@ static void solver_solve_velocity(Solver* s) {
             b = vsub(b, mat_mul(vc->K, a));
             for (;;) {
                 V2 x = vneg(mat_mul(vc->nm, b));
-                if (x.x >= 0.0f && x.y >= 0.0f) goto apply;
+                if (x.x >= 0.0f && x.y >= 0.0f) { LCP_CASE(0); goto apply; }
                 x.x = -cp1->normalMass * b.x; x.y = 0.0f;
                 vn1 = 0.0f; vn2 = vc->K[1] * x.x + b.y;
-                if (x.x >= 0.0f && vn2 >= 0.0f) goto apply;
+                if (x.x >= 0.0f && vn2 >= 0.0f) { LCP_CASE(1); goto apply; }
                 x.x = 0.0f; x.y = -cp2->normalMass * b.y;
                 vn1 = vc->K[2] * x.y + b.x; vn2 = 0.0f;
-                if (x.y >= 0.0f && vn1 >= 0.0f) goto apply;
+                if (x.y >= 0.0f && vn1 >= 0.0f) { LCP_CASE(2); goto apply; }
                 x.x = 0.0f; x.y = 0.0f; vn1 = b.x; vn2 = b.y;
-                if (vn1 >= 0.0f && vn2 >= 0.0f) goto apply;
+                if (vn1 >= 0.0f && vn2 >= 0.0f) { LCP_CASE(3); goto apply; }
+                LCP_CASE(4);
                 break;
             apply: {
                     V2 d = vsub(x, a);
@@ -1376,6 +1390,76 @@ static int work_velocity_sweeps(Solver* s, int iters, int nbodies) {
     return run >= 0 ? run : iters;
 }
 
+/* diagnostic (b2o_model_2wave): the island's `sweeps` velocity sweeps (device
+ * count, `iters` configured) priced on one wave, and split over two waves of one workgroup.  Each
+ * wave runs its contacts in the island's Gauss-Seidel order; a contact starts when its wave is free
+ * and every dynamic body it touches holds the value of the body's previous update in sequential order
+ * (+x cycles when that update ran on the other wave: an LDS handoff), so the split is bit-exact by
+ * construction.  At each early-exit compare point the waves meet (+b).  The partition (contact 0 on
+ * wave 0) is the best of all 2^(nc-1) for nc <= 12 over the first min(sweeps, 8) sweeps. */
+static double g2w_cost[16], g2w_x = -1.0, g2w_b = 0.0;
+void b2o_model_2wave(const double* cost16, double x, double b) {
+    if (!cost16) { g2w_x = -1.0; return; }
+    for (int i = 0; i < 16; ++i) g2w_cost[i] = cost16[i];
+    g2w_x = x; g2w_b = b;
+}
+static double twowave_run(const Solver* s, const int* dyn, int nb, unsigned mask, int sweeps, int iters, int barriers) {
+    double fin[256], tw[2] = {0.0, 0.0};
+    int own[256], n[2] = {0, 0};
+    for (int i = 0; i < s->count; ++i) ++n[(mask >> i) & 1u];
+    for (int k = 0; k < nb; ++k) { fin[k] = 0.0; own[k] = -1; }
+    int have = (iters & 3) == 2;
+    for (int r = 0; r < sweeps; ++r) {
+        for (int i = 0; i < s->count; ++i) {
+            const int w = (mask >> i) & 1u, ab[2] = {s->vcs[i].indexA, s->vcs[i].indexB};
+            double t = tw[w];
+            for (int j = 0; j < 2; ++j)
+                if (dyn[ab[j]] && own[ab[j]] >= 0) {
+                    const double ready = fin[ab[j]] + (own[ab[j]] != w ? g2w_x : 0.0);
+                    if (ready > t) t = ready;
+                }
+            const int nw = n[w] < 8 ? n[w] : 8, p = s->vcs[i].pointCount < 2 ? 0 : 1;
+            t += g2w_cost[p * 8 + nw - 1];
+            tw[w] = t;
+            for (int j = 0; j < 2; ++j)
+                if (dyn[ab[j]]) { fin[ab[j]] = t; own[ab[j]] = w; }
+        }
+        if (!barriers) continue;
+        const int done = r + 1, left = iters - done, m = exit_mask(done);
+        if ((left & m) == 0 && have) {
+            const double t = (tw[0] > tw[1] ? tw[0] : tw[1]) + g2w_b;
+            tw[0] = tw[1] = t;
+        }
+        if ((left & m) == 2) have = 1;
+    }
+    return tw[0] > tw[1] ? tw[0] : tw[1];
+}
+static void work_model_2wave(const Solver* s, const int* dyn, int sweeps, int iters, OrWork* k) {
+    if (g2w_x < 0.0 || s->count < 1) return;
+    int nb = 0;
+    for (int i = 0; i < s->count; ++i) {
+        if (s->vcs[i].indexA + 1 > nb) nb = s->vcs[i].indexA + 1;
+        if (s->vcs[i].indexB + 1 > nb) nb = s->vcs[i].indexB + 1;
+    }
+    if (nb > 256) return;
+    const double one = twowave_run(s, dyn, nb, 0u, sweeps, iters, 0);
+    double two = one;
+    if (s->count >= 2 && s->count <= 12) {
+        unsigned best = 0u;
+        double bt = 0.0;
+        const int probe = sweeps < 8 ? sweeps : 8;
+        for (unsigned m = 0; m < (1u << (s->count - 1)); ++m) {
+            const unsigned mask = m << 1;   /* contact 0 stays on wave 0 */
+            const double t = twowave_run(s, dyn, nb, mask, probe, iters, 0);
+            if (m == 0 || t < bt) { bt = t; best = mask; }
+        }
+        two = twowave_run(s, dyn, nb, best, sweeps, iters, 1);
+        if (best == 0u || two > one) two = one;   /* a split that does not pay stays on one wave */
+    }
+    k->vel_1wave += (long)(one + 0.5);
+    k->vel_2wave += (long)(two + 0.5);
+}
+
 /* diagnostic (b2o_topo_diag(1); b2o_topo_diag(2) also records 1- and 2-contact islands): island
  * topologies of 3- and 4-contact islands, weighted by sweeps run:
  * per contact (A slot, B slot, point count) with body slots numbered by first appearance and static
@@ -1404,7 +1488,32 @@ static void topo_record(const Solver* s, const Island* is, int sweeps) {
         if (k < 64) { g_topo_sig[k] = sig; g_topo_w[k] += sweeps * (long)s->count; }
     }
 }
+/* b2o_topo_diag(3): print (stderr, first 60) the contact list of islands with >= 5 contacts that run
+ * >= 100 sweeps: per contact "A-B/points", body slots by first appearance, static bodies as S */
+static int g_topo_printed = 0;
+static void topo_print(const Solver* s, const Island* is, int sweeps) {
+    char buf[512];
+    int slot[256], ns = 0, n = 0;
+    for (int k = 0; k < 256; ++k) slot[k] = -1;
+    n += snprintf(buf + n, sizeof(buf) - n, "nc %d sweeps %3d:", s->count, sweeps);
+    for (int i = 0; i < s->count && n < 480; ++i) {
+        const int ab[2] = {s->vcs[i].indexA, s->vcs[i].indexB};
+        char c[2];
+        for (int j = 0; j < 2; ++j) {
+            const Body* b = is->bodies[ab[j]];
+            if (b->invMass == 0.0f && b->invI == 0.0f) { c[j] = 'S'; continue; }
+            if (slot[ab[j]] < 0) slot[ab[j]] = ns++;
+            c[j] = (char)('0' + slot[ab[j]]);
+        }
+        n += snprintf(buf + n, sizeof(buf) - n, " %c-%c/%d", c[0], c[1], s->vcs[i].pointCount);
+    }
+#pragma omp critical
+    {
+        if (g_topo_printed < 100000) { fprintf(stderr, "%s\n", buf); ++g_topo_printed; }
+    }
+}
 void b2o_topo_diag(int on, long* sig64, long* w64) {
+    g_topo_printed = 0;
     for (int k = 0; k < 64; ++k) { if (sig64) sig64[k] = g_topo_sig[k]; if (w64) w64[k] = g_topo_w[k]; }
     if (on >= 0) { g_topo_diag = on; for (int k = 0; k < 64; ++k) { g_topo_sig[k] = 0; g_topo_w[k] = 0; } }
 }
@@ -1498,7 +1607,8 @@ static void island_solve(Island* is, World* w, TimeStep step) {
         ++passes;
         if (solver_solve_position(&s, 0, -1, -1)) break;
     }
-    if (g_topo_diag && is->contactCount >= (g_topo_diag > 1 ? 1 : 3) && is->contactCount <= 4) topo_record(&s, is, sweeps);
+    if (g_topo_diag && g_topo_diag < 3 && is->contactCount >= (g_topo_diag > 1 ? 1 : 3) && is->contactCount <= 4) topo_record(&s, is, sweeps);
+    if (g_topo_diag == 3 && is->contactCount >= 5 && sweeps >= 100) topo_print(&s, is, sweeps);
     if (is->contactCount > 0) {
         int dyn[256], lp = 0, pts = 0, n1 = 0, n2 = 0;
         for (int k = 0; k < is->bodyCount && k < 256; ++k) dyn[k] = is->bodies[k]->invMass > 0.0f || is->bodies[k]->invI > 0.0f;
@@ -1510,6 +1620,7 @@ static void island_solve(Island* is, World* w, TimeStep step) {
         k->pos_passes += passes; k->pos_points += (long)passes * pts; k->pos_level_points += (long)passes * lp;
         k->vel_pipe += work_pipe(&s, dyn, sweeps, 0);
         k->pos_pipe += work_pipe(&s, dyn, passes, 1);
+        work_model_2wave(&s, dyn, sweeps, step.velocityIterations, k);
         const long units = (long)sweeps * s.count + (long)passes * pts;
         k->isl_units += units;
         w->stepIslSum += units;

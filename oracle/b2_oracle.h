@@ -128,7 +128,9 @@ typedef struct {
     long isl_units;                      /* discrete islands' velocity updates + position points */
     long isl_concurrent_save;            /* per step: those units minus the largest island's (what solving a
                                           * step's independent islands concurrently would take off the chain) */
-    long reserved[2];
+    long vel_1wave, vel_2wave;           /* b2o_model_2wave (off: 0): modelled cycles of the discrete islands'
+                                          * velocity sweeps on one wave, and split over two waves of one
+                                          * workgroup (best contact partition, LDS handoffs priced) */
 } OrWork;
 
 enum { WF_NEWFIXTURE = 1, WF_LOCKED = 2, WF_CLEARFORCES = 4 };
@@ -172,6 +174,11 @@ void b2o_set_listener(World* w, ContactCb begin, ContactCb end, void* ctx);
 void b2o_period_diag(int on, long* out300);
 /* diagnostic: the work model counts velocity sweeps as if periods up to p were detected (0 = the device) */
 void b2o_model_period(int p);
+/* diagnostic: price the velocity sweeps on one wave and split over two (OrWork vel_1wave /
+ * vel_2wave); cost[(p - 1) * 8 + n - 1] = cycles of one p-point contact update on a wave holding n
+ * contacts (n > 8 priced as 8), x = cycles of one cross-wave handoff, b = cycles of the two waves'
+ * joint early-exit compare; cost NULL switches the model off */
+void b2o_model_2wave(const double* cost16, double x, double b);
 /* diagnostic: topology histogram of 3- and 4-contact islands (see b2_oracle.c) */
 void b2o_topo_diag(int on, long* sig64, long* w64);
 

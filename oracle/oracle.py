@@ -250,8 +250,8 @@ def batch_capacity(env_id: int, lanes: int, steps: int, seed: int, bounds, threa
 
 WORK_NAMES = ("islands", "vel_sweeps", "vel_upd1", "vel_upd2", "vel_levels", "pos_passes", "pos_points",
               "pos_level_points", "toi_vel_upd", "toi_vel_levels", "toi_pos_points", "toi_pos_level_points",
-              "sat_calls", "toi_calls", "vel_pipe", "pos_pipe", "isl_units", "isl_concurrent_save", "reserved0",
-              "reserved1")
+              "sat_calls", "toi_calls", "vel_pipe", "pos_pipe", "isl_units", "isl_concurrent_save", "vel_1wave",
+              "vel_2wave")
 
 
 def batch_work(env_id: int, lanes: int, steps: int, seed: int, bounds, threads: int = 1, max_steps: int = 0) -> np.ndarray:

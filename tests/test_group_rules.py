@@ -108,3 +108,53 @@ def test_sparse_exit_schedule_is_exact(pairs):
                 assert (iters - k) % 2 == 0
             if left & m == 2:
                 snap_at = k
+
+
+# ----------------------------------------------------------------------------- branch-free block solver
+def _block_sequential(x1, b, nmass0, nmass1, k1):
+    """b2ContactSolver::SolveVelocityConstraints' 2-point block solver case loop (mrp_world.h
+    vel_update_m, case by case): the first case that holds gives x; None = no case holds."""
+    f = lambda v: f32(v)  # noqa: E731
+    if x1[0] >= 0.0 and x1[1] >= 0.0:
+        return x1
+    x = (f(f(-nmass0) * b[0]), 0.0)
+    vn2 = f(f(k1 * x[0]) + b[1])
+    if x[0] >= 0.0 and vn2 >= 0.0:
+        return x
+    x = (0.0, f(f(-nmass1) * b[1]))
+    vn1 = f(f(k1 * x[1]) + b[0])
+    if x[1] >= 0.0 and vn1 >= 0.0:
+        return x
+    if b[0] >= 0.0 and b[1] >= 0.0:
+        return (0.0, 0.0)
+    return None
+
+
+def _block_selects(x1, b, nmass0, nmass1, k1):
+    """The branch-free form (MRP_VEL_BFREE): all cases evaluated, picked by selects, one 'ok' mask."""
+    f = lambda v: f32(v)  # noqa: E731
+    x2 = f(f(-nmass0) * b[0]); v2 = f(f(k1 * x2) + b[1])
+    x3 = f(f(-nmass1) * b[1]); v3 = f(f(k1 * x3) + b[0])
+    c1 = x1[0] >= 0.0 and x1[1] >= 0.0
+    c2 = x2 >= 0.0 and v2 >= 0.0
+    c3 = x3 >= 0.0 and v3 >= 0.0
+    c4 = b[0] >= 0.0 and b[1] >= 0.0
+    xs = (x1[0] if c1 else (x2 if c2 else 0.0), x1[1] if c1 else (0.0 if c2 else (x3 if c3 else 0.0)))
+    return xs if (c1 or c2 or c3 or c4) else None
+
+
+def test_branch_free_block_solver_equals_case_loop():
+    """Same impulse bits (signed zeros included) or the same 'no solution' for random, signed-zero,
+    NaN, infinite and subnormal inputs of the case tests."""
+    rng = random.Random(9)
+    special = [0.0, -0.0, 1e-45, -1e-45, float("nan"), float("inf"), -float("inf"), 1.0, -1.0, 3.0e38]
+    def val():
+        return rng.choice(special) if rng.random() < 0.3 else f32(rng.uniform(-2, 2) * 10 ** rng.randint(-6, 3))
+    for _ in range(200000):
+        x1, b = (val(), val()), (val(), val())
+        nm0, nm1, k1 = f32(abs(val())), f32(abs(val())), val()
+        s = _block_sequential(x1, b, nm0, nm1, k1)
+        t = _block_selects(x1, b, nm0, nm1, k1)
+        assert (s is None) == (t is None), (x1, b, nm0, nm1, k1)
+        if s is not None:
+            assert bits(s[0]) + bits(s[1]) == bits(t[0]) + bits(t[1]), (x1, b, nm0, nm1, k1, s, t)

@@ -24,6 +24,11 @@ for lib in gym_puzzles_amd/libmrp.so $LIBS; do
     || { echo "velbench failed ($lib)"; tail "$OUT/velbench_$(basename $lib .so).txt"; exit 1; }
   grep "blocks     1" "$OUT/velbench_$(basename $lib .so).txt" | sed "s/^/$(basename $lib .so): /"
 done
+for lib in gym_puzzles_amd/libmrp.so $LIBS; do
+  MRP_LIB=$lib timeout -k 10 120 python -u tools/posbench.py > "$OUT/posbench_$(basename $lib .so).txt" 2>&1 \
+    || { echo "posbench failed ($lib)"; tail "$OUT/posbench_$(basename $lib .so).txt"; exit 1; }
+  grep "blocks     1" "$OUT/posbench_$(basename $lib .so).txt" | sed "s/^/$(basename $lib .so): /"
+done
 if [ "$BENCH" = 1 ]; then
   for lib in gym_puzzles_amd/libmrp.so $LIBS; do
     MRP_LIB=$lib timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --single-env 0 --later-window 0 --episode 0 --multi-step 0 > "$OUT/bench_drv_$(basename $lib .so).log" 2>&1 \

@@ -12,7 +12,7 @@ L = _native.load()
 iters = 180
 for blocks in (1, 1024, 4096):
     # nc >= 100: a chain of nc - 100 contacts (contact i between bodies i and i + 1)
-    for nc, pc in ((1, 1), (1, 2), (2, 2), (3, 2), (4, 2), (6, 2), (104, 2), (106, 2)):
+    for nc, pc in ((1, 1), (1, 2), (2, 2), (3, 2), (4, 2), (6, 2), (104, 2), (106, 2), (2, 1), (3, 1), (4, 1), (6, 1)):
         out = np.zeros(blocks, np.uint64)
         rc = L.mrp_debug_velbench(0, nc, pc, iters, blocks, out.ctypes.data)
         if rc != 0 and nc >= 100:
