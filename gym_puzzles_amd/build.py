@@ -48,8 +48,14 @@ _GRANULES = ["-DMRP_CONTACT_GRANULES=1"]
 # steps 21-220, v3 +4.9 % / +4.4 %; Heavy-v0 -2 %, the 3-block config -1.7 % and v2 -2.5 % (against
 # max-ilp) under it, so those keep their choices (profiles/r4_ab_sched_iterative_ilp.txt).
 _ITER_ILP = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
-UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS + _ITER_ILP, "mrp_env1.hip": _MAX_ILP, "mrp_env2.hip": _GRANULES + _MAX_ILP,
-              "mrp_env4.hip": _ILP_LOOPS, "mrp_env5.hip": _LANES_PAIRS + _ITER_ILP}
+# Round 5 (profiles/r5_ab_bfree_xw.txt): v2 and the 3-block config pick the block solver's case
+# without a chain of case tests (MRP_VEL_BFREE, with the two-ballot case test and the tangent speed as
+# a cross product): their slowest lane-steps replayed alone +0.8 % / +3.3 %, bitwise; v0 -0.1 % (the
+# selects and ballots add to every two-point update what the saved case tests take off), so v0 keeps
+# the case loop.
+_BFREE = ["-DMRP_VEL_BFREE=1", "-DMRP_VEL_PICK2=1", "-DMRP_VEL_VTCROSS=1"]
+UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS + _ITER_ILP, "mrp_env1.hip": _MAX_ILP, "mrp_env2.hip": _GRANULES + _MAX_ILP + _BFREE,
+              "mrp_env4.hip": _ILP_LOOPS + _BFREE, "mrp_env5.hip": _LANES_PAIRS + _ITER_ILP}
 # -fno-slp-vectorize: the serial solver chains are latency-bound; packing pairs of f32 ops into
 # v_pk_* costs operand-shuffling moves on the dependency chain (measured +2-3 % env-steps/s off)
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",

@@ -228,6 +228,9 @@ struct StateIO {
 #ifndef MRP_CONTACT_GRANULES
 #define MRP_CONTACT_GRANULES 0
 #endif
+#ifndef MRP_FRESH_REGS
+#define MRP_FRESH_REGS 0
+#endif
     using Contacts = typename std::conditional<MRP_CONTACT_GRANULES != 0, ContactGranules, ContactWords>::type;
     // hw_io <- the loaded cHW (clamped to the pool; kept in LDS, not live in registers across the step)
     __device__ __forceinline__ static void load(LS& S, int& hw_io, const uint32_t* __restrict__ gs, int lane, int tid) {
@@ -247,6 +250,12 @@ struct StateIO {
         if (tid == 0) hw_io = hw;
     }
     __device__ __forceinline__ static void store(const LS& S, const int& hw_io, uint32_t* __restrict__ gs, int lane, int tid) {
+#if MRP_FRESH_REGS
+        // the per-thread word offsets recomputed here from an opaque copy of the thread id, not kept
+        // live from the load at entry (v0 under the iterative-ilp schedule spilled two of them to
+        // scratch across the whole step)
+        asm volatile("" : "+v"(tid));
+#endif
         word_t* g = gs + (size_t)lane * NW;
         word_t* lds = const_cast<word_t*>(reinterpret_cast<const word_t*>(&S));
         const int hw = max(hw_io, min(max(S.cHW, 0), C));

@@ -95,6 +95,12 @@ constexpr int NULLN = -1;
 #ifndef MRP_VEL_BFREE
 #define MRP_VEL_BFREE 0
 #endif
+// MRP_FRESH_REGS=1: values k_step needs late in the step (the state store's per-thread offsets, the
+// TOI phase's zeroes) are made where they are used, so they are not live across the step (v0 spilled
+// them to scratch: 8 of its 14 VGPR spills)
+#ifndef MRP_FRESH_REGS
+#define MRP_FRESH_REGS 0
+#endif
 #if MRP_VEL_EXPECT
 #define MRP_UNLIKELY(c) __builtin_expect(!!(c), 0)
 #define MRP_LIKELY(c) __builtin_expect(!!(c), 1)
@@ -2786,8 +2792,16 @@ template <int ENV> struct World {
     }
     __device__ __forceinline__ void solve_toi_coop(float dt) {
         if (tid == 0) {
-            for (int i = 0; i < 4; ++i) sh.salpha0[i] = 0.0f;
-            for (int b = 0; b < ND; ++b) S.alpha0[b] = 0.0f;
+#if MRP_FRESH_REGS
+            // the zero made here (v_mov), not a copy of one made at k_step's entry: under v0's
+            // iterative-ilp schedule those copies lived across the step in scratch
+            float zero;
+            asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+#else
+            const float zero = 0.0f;
+#endif
+            for (int i = 0; i < 4; ++i) sh.salpha0[i] = zero;
+            for (int b = 0; b < ND; ++b) S.alpha0[b] = zero;
             for (int c = S.cHead, g_ = 0; c != NULLN && list_ok(g_); c = S.cnext[c]) { S.cflags[c] &= ~(CF_TOI | CF_ISLAND); S.ctoiCount[c] = 0; S.ctoi[c] = 1.0f; }
             sh.toi_done = 0;
         }

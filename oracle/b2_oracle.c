@@ -1397,9 +1397,13 @@ static int work_velocity_sweeps(Solver* s, int iters, int nbodies) {
  * (+x cycles when that update ran on the other wave: an LDS handoff), so the split is bit-exact by
  * construction.  At each early-exit compare point the waves meet (+b).  The partition (contact 0 on
  * wave 0) is the best of all 2^(nc-1) for nc <= 12 over the first min(sweeps, 8) sweeps. */
-static double g2w_cost[16], g2w_x = -1.0, g2w_b = 0.0;
+static double g2w_cost[16], g2w_x = -1.0, g2w_b = 0.0, g2w_read = 0.0, g2w_pub = 0.0;
 void b2o_model_2wave(const double* cost16, double x, double b) {
     if (!cost16) { g2w_x = -1.0; return; }
+    /* OR_2W_READ / OR_2W_PUB: cycles a cross-wave dependency adds to the consumer's update (its LDS
+     * read of the body) and to the producer's (the LDS write + flag), waiting or not */
+    g2w_read = getenv("OR_2W_READ") ? atof(getenv("OR_2W_READ")) : 0.0;
+    g2w_pub = getenv("OR_2W_PUB") ? atof(getenv("OR_2W_PUB")) : 0.0;
     for (int i = 0; i < 16; ++i) g2w_cost[i] = cost16[i];
     g2w_x = x; g2w_b = b;
 }
@@ -1412,14 +1416,24 @@ static double twowave_run(const Solver* s, const int* dyn, int nb, unsigned mask
     for (int r = 0; r < sweeps; ++r) {
         for (int i = 0; i < s->count; ++i) {
             const int w = (mask >> i) & 1u, ab[2] = {s->vcs[i].indexA, s->vcs[i].indexB};
-            double t = tw[w];
+            double t = tw[w], rd = 0.0, pub = 0.0;
             for (int j = 0; j < 2; ++j)
                 if (dyn[ab[j]] && own[ab[j]] >= 0) {
                     const double ready = fin[ab[j]] + (own[ab[j]] != w ? g2w_x : 0.0);
+                    if (own[ab[j]] != w) rd = g2w_read;   /* the LDS read of a body the other wave wrote */
                     if (ready > t) t = ready;
                 }
+            for (int j = 0; j < 2 && mask; ++j)   /* publishing a body the other wave updates next */
+                if (dyn[ab[j]]) {
+                    int nx = -1;
+                    for (int q = 1; q <= s->count && nx < 0; ++q) {
+                        const int k2 = (i + q) % s->count;
+                        if (s->vcs[k2].indexA == ab[j] || s->vcs[k2].indexB == ab[j]) nx = k2;
+                    }
+                    if (nx >= 0 && (int)((mask >> nx) & 1u) != w) pub = g2w_pub;
+                }
             const int nw = n[w] < 8 ? n[w] : 8, p = s->vcs[i].pointCount < 2 ? 0 : 1;
-            t += g2w_cost[p * 8 + nw - 1];
+            t += rd + pub + g2w_cost[p * 8 + nw - 1];
             tw[w] = t;
             for (int j = 0; j < 2; ++j)
                 if (dyn[ab[j]]) { fin[ab[j]] = t; own[ab[j]] = w; }
@@ -1434,8 +1448,85 @@ static double twowave_run(const Solver* s, const int* dyn, int nb, unsigned mask
     }
     return tw[0] > tw[1] ? tw[0] : tw[1];
 }
+/* Paired contact updates on one wave (b2o_model_dual): the island's Gauss-Seidel stream of
+ * `D` sweeps (item q = sweep q / nc, contact q % nc) cut into slots of one or two updates run by one
+ * instruction stream in two lanes.  Greedy, in stream order: a slot takes the first unscheduled item
+ * u and the first unscheduled item v after it (at most `window` items on) with u's point count that
+ * shares no dynamic body with u nor with any unscheduled item between them -- so every body and
+ * every contact sees its updates in the sequential order and the result is bit-exact.  out[t] =
+ * u | v << 4 (v == u: a single); returns the slot count (or -1 when `cap` is too small). */
+static int g_dual_mixed = 0;   /* model only: pairs of any point counts */
+int b2o_dual_schedule(int nc, const int* ia, const int* ib, const int* dyn, const int* pcount, int D, int window,
+                      unsigned char* out, int cap) {
+    const int n = nc * D;
+    unsigned char done[2048];
+    if (n > 2048 || nc > 15) return -1;
+    for (int q = 0; q < n; ++q) done[q] = 0;
+    int t = 0, u = 0;
+#define CONFL(p, q) ((dyn[ia[(p) % nc]] && (ia[(p) % nc] == ia[(q) % nc] || ia[(p) % nc] == ib[(q) % nc])) || \
+                     (dyn[ib[(p) % nc]] && (ib[(p) % nc] == ia[(q) % nc] || ib[(p) % nc] == ib[(q) % nc])))
+    while (u < n) {
+        done[u] = 1;
+        int v = u;
+        for (int q = u + 1; q < n && q <= u + window; ++q) {
+            if (done[q] || (!g_dual_mixed && pcount[q % nc] != pcount[u % nc]) || CONFL(u, q)) continue;
+            int ok = 1;
+            for (int r = u + 1; r < q && ok; ++r)
+                if (!done[r] && CONFL(r, q)) ok = 0;
+            if (ok) { v = q; break; }
+        }
+        done[v] = 1;
+        if (t >= cap) return -1;
+        out[t++] = (unsigned char)((u % nc) | ((v % nc) << 4));
+        while (u < n && done[u]) ++u;
+    }
+#undef CONFL
+    return t;
+}
+static double g_dual_factor = 0.0;
+static int g_dual_window = 0, g_dual_nodrain = 0;
+/* window < 0: |window|, and the stream never drains (the bound without early-exit meeting points) */
+void b2o_model_dual(double factor, int window) {
+    g_dual_factor = factor; g_dual_window = window < 0 ? -window : window; g_dual_nodrain = window < 0;
+    g_dual_mixed = getenv("OR_DUAL_MIXED") != NULL;
+}
+/* the sweeps as the paired path would run them: segments between the early-exit events (snapshot
+ * and compare sweeps, where the stream drains), each slot priced as one update x factor */
+static double dual_run(const Solver* s, const int* dyn, int sweeps, int iters) {
+    const int nc = s->count;
+    int ia[16], ib[16], pc[16];
+    for (int i = 0; i < nc; ++i) { ia[i] = s->vcs[i].indexA; ib[i] = s->vcs[i].indexB; pc[i] = s->vcs[i].pointCount; }
+    unsigned char sl[2048];
+    double t = 0.0;
+    int k = 0;
+    while (k < sweeps) {
+        int e = g_dual_nodrain ? sweeps : k + 1;   /* next event sweep (or the end) */
+        while (e < sweeps) {
+            const int left = iters - e, m = exit_mask(e);
+            if ((left & m) == 0 || (left & m) == 2) break;
+            ++e;
+        }
+        const int D = e - k;
+        const int ns = b2o_dual_schedule(nc, ia, ib, dyn, pc, D, g_dual_window, sl, 2048);
+        if (ns < 0) return -1.0;
+        for (int q = 0; q < ns; ++q) {
+            const int u = sl[q] & 15, p = pc[u] < 2 ? 0 : 1;
+            t += g2w_cost[p * 8 + (nc < 8 ? nc : 8) - 1] * g_dual_factor;
+        }
+        k = e;
+    }
+    return t;
+}
 static void work_model_2wave(const Solver* s, const int* dyn, int sweeps, int iters, OrWork* k) {
     if (g2w_x < 0.0 || s->count < 1) return;
+    if (g_dual_factor > 0.0) {   /* b2o_model_dual: vel_2wave holds the paired one-wave path */
+        const double one = twowave_run(s, dyn, 256, 0u, sweeps, iters, 0);
+        double d = s->count >= 3 && s->count <= 15 ? dual_run(s, dyn, sweeps, iters) : one;
+        if (d < 0.0) d = one;
+        k->vel_1wave += (long)(one + 0.5);
+        k->vel_2wave += (long)(d + 0.5);
+        return;
+    }
     int nb = 0;
     for (int i = 0; i < s->count; ++i) {
         if (s->vcs[i].indexA + 1 > nb) nb = s->vcs[i].indexA + 1;

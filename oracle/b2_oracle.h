@@ -179,6 +179,12 @@ void b2o_model_period(int p);
  * contacts (n > 8 priced as 8), x = cycles of one cross-wave handoff, b = cycles of the two waves'
  * joint early-exit compare; cost NULL switches the model off */
 void b2o_model_2wave(const double* cost16, double x, double b);
+/* diagnostic: with factor > 0, vel_2wave prices the paired one-wave path instead (slots of one or two
+ * same-point-count updates, b2o_dual_schedule, each priced as one update x factor); 0 switches it off */
+void b2o_model_dual(double factor, int window);
+/* the paired path's slot schedule of D sweeps of an nc-contact island (see b2_oracle.c) */
+int b2o_dual_schedule(int nc, const int* ia, const int* ib, const int* dyn, const int* pcount, int D, int window,
+                      unsigned char* out, int cap);
 /* diagnostic: topology histogram of 3- and 4-contact islands (see b2_oracle.c) */
 void b2o_topo_diag(int on, long* sig64, long* w64);
 

@@ -93,6 +93,18 @@ def main():
         print(f"handoff {x:6.0f} cycles{tag}: slowest lane-steps one wave {m1 / 1e6:7.2f} Mcyc, two waves {m2 / 1e6:7.2f} Mcyc "
               f"(x{m1 / m2:.3f}); velocity share of the one-wave slowest lane-step {vel_share:.2f}; "
               f"all lanes' sweeps x{w[..., W['vel_1wave']].sum() / max(w[..., W['vel_2wave']].sum(), 1):.3f}")
+    L.b2o_model_dual.argtypes = [ctypes.c_double, ctypes.c_int]
+    for factor, window in ((1.0, -16), (1.0, 16), (1.1, 16), (1.2, 16)):   # paired updates on one wave: no handoff, each slot dearer
+        L.b2o_model_2wave(cbuf, 0.0, 0.0)
+        L.b2o_model_dual(factor, window)
+        w = batch_work(env, lanes, s1, 17, draw_bounds(env), threads=os.cpu_count() or 1)[s0 - 1:s1]
+        other = (C_FIX + C_POS * (w[..., W["pos_points"]] + w[..., W["toi_pos_points"]])
+                 + C_VEL * w[..., W["toi_vel_upd"]] + C_TOI * (w[..., W["toi_vel_upd"]] > 0))
+        one, two = other + w[..., W["vel_1wave"]], other + w[..., W["vel_2wave"]]
+        m1, m2 = one.max(axis=1).sum(), two.max(axis=1).sum()
+        print(f"paired lanes{' (no drains)' if window < 0 else ''}, slot = {factor:.1f} updates: slowest lane-steps one wave {m1 / 1e6:7.2f} Mcyc, paired {m2 / 1e6:7.2f} Mcyc "
+              f"(x{m1 / m2:.3f}); all lanes' sweeps x{w[..., W['vel_1wave']].sum() / max(w[..., W['vel_2wave']].sum(), 1):.3f}")
+    L.b2o_model_dual(0.0, 0)
     L.b2o_model_2wave(None, 0.0, 0.0)
 
 
