@@ -178,7 +178,7 @@ def load_valu(env_id: int, lanes: int, first: int, last: int, seed: int, kern_ms
             "source": "oracle op counts of this exact workload (tools/roofline_model.py, profiles/r3_valu_latency.json)"}
 
 
-ISSUE_TABLE = "r4_issue_roofline.json"
+ISSUE_TABLE = "r5_issue_roofline.json"
 
 
 def load_issue(env_id: int, lanes: int, first: int, last: int, seed: int, kern_ms: float):

@@ -54,7 +54,12 @@ _ITER_ILP = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
 # selects and ballots add to every two-point update what the saved case tests take off), so v0 keeps
 # the case loop.
 _BFREE = ["-DMRP_VEL_BFREE=1", "-DMRP_VEL_PICK2=1", "-DMRP_VEL_VTCROSS=1"]
-UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS + _ITER_ILP, "mrp_env1.hip": _MAX_ILP, "mrp_env2.hip": _GRANULES + _MAX_ILP + _BFREE,
+# v0 makes the values its step needs late (the state store's per-thread offsets, the TOI phase's
+# zeroes) where they are used (-DMRP_FRESH_REGS=1): VGPR spills 14 -> 4, scratch 48 -> 16 B per
+# thread, PMC traffic 30.9 -> 23.2 MB per launch; driver window -0.4 %, steps 21-220 -0.2 %, whole
+# episode +0.7 % (profiles/r5_windows_traffic_fresh.txt).
+_FRESH = ["-DMRP_FRESH_REGS=1"]
+UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS + _ITER_ILP + _FRESH, "mrp_env1.hip": _MAX_ILP, "mrp_env2.hip": _GRANULES + _MAX_ILP + _BFREE,
               "mrp_env4.hip": _ILP_LOOPS + _BFREE, "mrp_env5.hip": _LANES_PAIRS + _ITER_ILP}
 # -fno-slp-vectorize: the serial solver chains are latency-bound; packing pairs of f32 ops into
 # v_pk_* costs operand-shuffling moves on the dependency chain (measured +2-3 % env-steps/s off)

@@ -24,7 +24,7 @@
 #error "define MRP_ENV (the env id this translation unit instantiates)"
 #endif
 #ifdef MRP_STAMPS
-static_assert(MRP_TRACE_W == MRP_TRACE_WORDS, "the trace row width is part of the C ABI (mrp_debug_trace)");
+static_assert(mrp::MRP_TRACE_W == MRP_TRACE_WORDS, "the trace row width is part of the C ABI (mrp_debug_trace)");
 #endif
 
 using namespace mrp;
