@@ -158,3 +158,48 @@ def test_branch_free_block_solver_equals_case_loop():
         assert (s is None) == (t is None), (x1, b, nm0, nm1, k1)
         if s is not None:
             assert bits(s[0]) + bits(s[1]) == bits(t[0]) + bits(t[1]), (x1, b, nm0, nm1, k1, s, t)
+
+
+# ----------------------------------------------------------------------------- paired-slot schedule
+def test_dual_schedule_keeps_every_body_in_sequential_order():
+    """b2o_dual_schedule (the paired-update model of the 3-block accounting, oracle/b2_oracle.c):
+    replaying its slots must give every dynamic body the same sequence of updates, and every contact
+    its sweeps in order, as the Gauss-Seidel stream; a slot's two updates never share a dynamic body
+    and have one point count."""
+    import ctypes
+
+    from oracle.oracle import lib
+    L = lib()
+    L.b2o_dual_schedule.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_int] * 2 + [ctypes.c_void_p, ctypes.c_int]
+    L.b2o_dual_schedule.restype = ctypes.c_int
+    rng = random.Random(5)
+    arr = lambda v: (ctypes.c_int * len(v))(*v)  # noqa: E731
+    for _ in range(300):
+        nb, nc, D = rng.randint(2, 6), rng.randint(2, 8), rng.choice((1, 2, 3, 14))
+        dyn = [1] * (nb - 1) + [0]                          # the last body static (a wall)
+        ia = [rng.randrange(nb - 1) for _ in range(nc)]
+        ib = [rng.randrange(nb) for _ in range(nc)]
+        ib = [b if b != a else nb - 1 for a, b in zip(ia, ib)]
+        pc = [rng.randint(1, 2) for _ in range(nc)]
+        out = (ctypes.c_ubyte * 4096)()
+        ns = L.b2o_dual_schedule(nc, arr(ia), arr(ib), arr(dyn), arr(pc), D, 16, out, 4096)
+        assert 0 < ns <= nc * D
+        # sequential: per body, the list of contact indices that update it, sweep by sweep
+        seq = {b: [i for _ in range(D) for i in range(nc) if dyn[b] and b in (ia[i], ib[i])] for b in range(nb)}
+        got = {b: [] for b in range(nb)}
+        sweeps_run = [0] * nc
+        n_upd = 0
+        for t in range(ns):
+            u, v = out[t] & 15, out[t] >> 4
+            upd = [u] if u == v else [u, v]
+            if len(upd) == 2:
+                assert pc[u] == pc[v]
+                assert not ({b for b in (ia[u], ib[u]) if dyn[b]} & {b for b in (ia[v], ib[v]) if dyn[b]})
+            for i in upd:
+                sweeps_run[i] += 1
+                n_upd += 1
+                for b in {ia[i], ib[i]}:
+                    if dyn[b]:
+                        got[b].append(i)
+        assert n_upd == nc * D and sweeps_run == [D] * nc
+        assert got == seq
