@@ -52,14 +52,18 @@ _ITER_ILP = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
 # without a chain of case tests (MRP_VEL_BFREE, with the two-ballot case test and the tangent speed as
 # a cross product): their slowest lane-steps replayed alone +0.8 % / +3.3 %, bitwise; v0 -0.1 % (the
 # selects and ballots add to every two-point update what the saved case tests take off), so v0 keeps
-# the case loop.
+# the case loop; Heavy-v0 -1.0 % and v3 -4.9 % (profiles/r5_ab_bfree_env1_env5.txt) keep it too.
 _BFREE = ["-DMRP_VEL_BFREE=1", "-DMRP_VEL_PICK2=1", "-DMRP_VEL_VTCROSS=1"]
 # v0 makes the values its step needs late (the state store's per-thread offsets, the TOI phase's
 # zeroes) where they are used (-DMRP_FRESH_REGS=1): VGPR spills 14 -> 4, scratch 48 -> 16 B per
 # thread, PMC traffic 30.9 -> 23.2 MB per launch; driver window -0.4 %, steps 21-220 -0.2 %, whole
 # episode +0.7 % (profiles/r5_windows_traffic_fresh.txt).
 _FRESH = ["-DMRP_FRESH_REGS=1"]
-UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS + _ITER_ILP + _FRESH, "mrp_env1.hip": _MAX_ILP, "mrp_env2.hip": _GRANULES + _MAX_ILP + _BFREE,
+# v0 also takes the two-ballot case test and the cross-product tangent speed (without the
+# branch-free selection): slowest lane-steps +1.4 %, driver window +1.2 %, steps 21-220 +0.1 %, a
+# whole episode -1.0 % (profiles/r5_ab_v0_pick2_vtcross.txt).
+_PICK2_VT = ["-DMRP_VEL_PICK2=1", "-DMRP_VEL_VTCROSS=1"]
+UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS + _ITER_ILP + _FRESH + _PICK2_VT, "mrp_env1.hip": _MAX_ILP, "mrp_env2.hip": _GRANULES + _MAX_ILP + _BFREE,
               "mrp_env4.hip": _ILP_LOOPS + _BFREE, "mrp_env5.hip": _LANES_PAIRS + _ITER_ILP}
 # -fno-slp-vectorize: the serial solver chains are latency-bound; packing pairs of f32 ops into
 # v_pk_* costs operand-shuffling moves on the dependency chain (measured +2-3 % env-steps/s off)
