@@ -5,7 +5,7 @@
 set -euo pipefail
 export TMPDIR=/tmp
 ENV=${ENV:-0}; LANES=${LANES:-4096}; STEPS=${STEPS:-20}; WARMUP=${WARMUP:-5}
-ARGS="--steps $STEPS --warmup $WARMUP --no-cpu-baseline --later-window 0 --episode 0 --multi-step 0 --single-env 0 --env $ENV --lanes $LANES"
+ARGS="--steps $STEPS --warmup $WARMUP --no-cpu-baseline --later-window 0 --episode 0 --multi-step 0 --single-env 0 --env $ENV --lanes $LANES ${EXTRA:-}"
 for lib in "$@"; do
   n=$(basename $lib .so)
   OUT=gpurun_out/traffic_$n
