@@ -77,9 +77,6 @@ constexpr int NULLN = -1;
 #ifndef MRP_XW_PAIRS
 #define MRP_XW_PAIRS 0
 #endif
-#ifndef MRP_XW_GATE
-#define MRP_XW_GATE 0
-#endif
 #ifndef MRP_VEL_PICK2
 #define MRP_VEL_PICK2 0
 #endif
@@ -1263,11 +1260,7 @@ template <int ENV> struct World {
         // pay its call (k_step's live registers saved around it), so short solves stay on the lanes path
         if constexpr (XW_LATE_OK) {
             const XwShape q = xw_shape(is, vcs);
-            // MRP_XW_GATE = g > 0: only lanes whose previous step cost more than the fraction of the
-            // slowest lane's that priority level g stands for (prio_floor, k_step's cost priority,
-            // schedule mode 2) take the register path: the launch's critical lanes, not every lane
-            // with a long solve
-            if (xw_supported(q.key) && prio_floor >= MRP_XW_GATE) {
+            if (xw_supported(q.key)) {
                 bool done = false;
                 const int k = lanes_sweeps<NC>(is, vcs, iters, early_exit, MRP_XW_LATE, &done);
                 if (done) return k;
