@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round 5: Heavy-v0 / v3 with the two-ballot case test and the cross-product tangent speed
+# (var/pv15.so) against the default library (slowest lane-steps alone), then v0's issue roofline and
+# phase table recaptured on the final library (var/stamps5.so: the stamps build of the v0 unit) and
+# v0's driver-window line with its CPU baselines.
+set -uo pipefail
+O=gpurun_out/r5sj
+mkdir -p $O
+( for i in $(seq 1 75); do date >> $O/heartbeat; sleep 15; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+export TMPDIR=/tmp
+STAMPS=gym_puzzles_amd/var/stamps5.so
+MRP_LIB=$STAMPS timeout -k 10 200 python tools/issue_capture.py 5 4096 5 20 $O/cap_env5.npz > $O/cap_env5.log 2>&1 || { echo "capture failed"; tail $O/cap_env5.log; exit 1; }
+MRP_LIB=$STAMPS timeout -k 10 200 python tools/issue_replay.py $O/cap_env5.npz $O/replay_stamps_env5.json > $O/replay_stamps_env5.log 2>&1 || { echo "replay failed"; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_VMEM SQ_WAVE_CYCLES \
+    --output-format csv -d $O/pmc_env5 -o pmc -- python3 tools/issue_replay.py $O/cap_env5.npz /tmp/r.json > $O/pmc_env5.log 2>&1 || { echo "pmc failed"; exit 1; }
+timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $O/kt_env5 -o kt -- python3 tools/issue_replay.py $O/cap_env5.npz /tmp/r.json 3 \
+    > $O/kt_env5.log 2>&1 || { echo "kt failed"; exit 1; }
+MRP_LIB=$STAMPS timeout -k 10 200 python tools/phase_profile.py 5 4096 5 20 $O/r5_phase_env5.json > $O/r5_phase_env5.txt 2>&1 || { echo "phase failed"; exit 1; }
+head -1 $O/r5_phase_env5.txt
+python3 tools/issue_roofline.py $O $O/issue_new.json 5 > $O/issue_roofline.txt || { echo "issue roofline failed"; exit 1; }
+python3 -c "import json; a=json.load(open('profiles/r5_issue_roofline.json')); b=json.load(open('$O/issue_new.json')); a={k: v for k, v in a.items() if not k.startswith('5:')}; a.update(b); json.dump(a, open('profiles/r5_issue_roofline.json', 'w'), indent=1)"
+cp profiles/r5_issue_roofline.json $O/
+exit 0
