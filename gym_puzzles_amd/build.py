@@ -53,7 +53,11 @@ _ITER_ILP = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
 # a cross product): their slowest lane-steps replayed alone +0.8 % / +3.3 %, bitwise; v0 -0.1 % (the
 # selects and ballots add to every two-point update what the saved case tests take off), so v0 keeps
 # the case loop; Heavy-v0 -1.0 % and v3 -4.9 % (profiles/r5_ab_bfree_env1_env5.txt) keep it too.
-_BFREE = ["-DMRP_VEL_BFREE=1", "-DMRP_VEL_PICK2=1", "-DMRP_VEL_VTCROSS=1"]
+# With the "any case holds" test as per-lane selects as well (-DMRP_VEL_BFREE=2: the impulse applied
+# unconditionally, each output selected, no ballot -> branch on the chain): v2 +2.8 % / +2.5 %,
+# 3-block +2.4 % / +2.6 % (slowest lane-steps / driver window) over the ballot form; v0 +1.1 % in the
+# driver window but -5 % over a whole episode (profiles/r5_ab_bfree2.txt), so v0 keeps the case loop.
+_BFREE = ["-DMRP_VEL_BFREE=2", "-DMRP_VEL_PICK2=1", "-DMRP_VEL_VTCROSS=1"]
 # v0 makes the values its step needs late (the state store's per-thread offsets, the TOI phase's
 # zeroes) where they are used (-DMRP_FRESH_REGS=1): VGPR spills 14 -> 4, scratch 48 -> 16 B per
 # thread, PMC traffic 30.9 -> 23.2 MB per launch; driver window -0.4 %, steps 21-220 -0.2 %, whole

@@ -1496,12 +1496,28 @@ template <int ENV> struct World {
             P2 xs;
             xs.x = c1 ? x.x : (c2 ? x2 : 0.0f);
             xs.y = c1 ? x.y : (c2 ? 0.0f : (c3 ? x3 : 0.0f));
+#if MRP_VEL_BFREE >= 2
+            // whether any case holds picked per lane as well: the impulse is applied unconditionally and
+            // each output selected between the applied and the incoming value (the same bits either
+            // way), so no ballot -> scalar -> branch sits on the chain.  Every lane decides from its
+            // own values, which is the decision the kept lane needs (PickUni: identical lanes;
+            // PickLane: lane i keeps contact i's own result)
+            const bool any = c1 || c2 || c3 || (b.x >= 0.0f && b.y >= 0.0f);
+            const P2 vA0 = vA, vB0 = vB, ni0 = ni;
+            const float wA0 = wA, wB0 = wB;
+            apply(xs);
+            vA.x = any ? vA.x : vA0.x; vA.y = any ? vA.y : vA0.y; wA = any ? wA : wA0;
+            vB.x = any ? vB.x : vB0.x; vB.y = any ? vB.y : vB0.y; wB = any ? wB : wB0;
+            ni.x = any ? ni.x : ni0.x; ni.y = any ? ni.y : ni0.y;
+            (void)pick;
+#else
             // some case holds (else Box2D gives up and leaves the contact unchanged): one ballot per compare
             const uint64_t ok = (__builtin_amdgcn_ballot_w64(x.x >= 0.0f) & __builtin_amdgcn_ballot_w64(x.y >= 0.0f)) |
                                 (__builtin_amdgcn_ballot_w64(x2 >= 0.0f) & __builtin_amdgcn_ballot_w64(v2 >= 0.0f)) |
                                 (__builtin_amdgcn_ballot_w64(x3 >= 0.0f) & __builtin_amdgcn_ballot_w64(v3 >= 0.0f)) |
                                 (__builtin_amdgcn_ballot_w64(b.x >= 0.0f) & __builtin_amdgcn_ballot_w64(b.y >= 0.0f));
             if (pick.mask(ok)) apply(xs);
+#endif
 #elif MRP_VEL_SPEC
             // case 1 (both points active) applied speculatively, its test resolved after the
             // application: the branch leaves the dependency chain.  When case 1 does not hold, the
