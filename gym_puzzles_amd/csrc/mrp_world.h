@@ -95,6 +95,9 @@ constexpr int NULLN = -1;
 #ifndef MRP_VEL_BFREE
 #define MRP_VEL_BFREE 0
 #endif
+#ifndef MRP_VEL_BFREE_LANES
+#define MRP_VEL_BFREE_LANES 0
+#endif
 // MRP_FRESH_REGS=1: values k_step needs late in the step (the state store's per-thread offsets, the
 // TOI phase's zeroes) are made where they are used, so they are not live across the step (v0 spilled
 // them to scratch: 8 of its 14 VGPR spills)
@@ -1342,6 +1345,7 @@ template <int ENV> struct World {
     // so each ballot is the v_cmp's own lane mask (no bool materialised in a VGPR and compared back)
     // and lane i's bit is one scalar bit test.
     struct PickUni {
+        static constexpr bool LANES = false;
         __device__ __forceinline__ bool operator()(bool c) const { return uni(c); }
         __device__ __forceinline__ bool mask(uint64_t m) const { return m != 0ull; }   // m: a ballot
         __device__ __forceinline__ bool both(bool a, bool b) const {
@@ -1353,6 +1357,7 @@ template <int ENV> struct World {
         }
     };
     struct PickLane {
+        static constexpr bool LANES = true;
         int i;
         __device__ __forceinline__ bool operator()(bool c) const { return lane_bit(c, i); }
         __device__ __forceinline__ bool mask(uint64_t m) const { return (m >> i) & 1ull; }
@@ -1485,39 +1490,58 @@ template <int ENV> struct World {
                 ni = xs;
             };
 #if MRP_VEL_BFREE
-            // All four cases evaluated at once and the first that holds picked by selects, in Box2D's
-            // order (both points active; point 1 only; point 2 only; none), so no case test waits on
-            // the one before it.  The launches' slowest lanes mostly run the later cases (v0: 72 %
-            // of their 2-point updates, v2: all; oracle b2o_lcp_cases on the captured lane-steps),
-            // which the case-by-case branches reach only after one to three failed tests.
-            const float x2 = -c.nmass0 * b.x, v2 = c.k01.y * x2 + b.y;   // case 2: x = (x2, 0), vn2 = k1 x2 + b.y
-            const float x3 = -c.nmass1 * b.y, v3 = c.k01.y * x3 + b.x;   // case 3: x = (0, x3), vn1 = k1 x3 + b.x
-            const bool c1 = x.x >= 0.0f && x.y >= 0.0f, c2 = x2 >= 0.0f && v2 >= 0.0f, c3 = x3 >= 0.0f && v3 >= 0.0f;
-            P2 xs;
-            xs.x = c1 ? x.x : (c2 ? x2 : 0.0f);
-            xs.y = c1 ? x.y : (c2 ? 0.0f : (c3 ? x3 : 0.0f));
+            // MRP_VEL_BFREE_LANES: the selects on the lanes path only (3+ contacts); the register paths
+            // (one and two contacts, mostly case-1 updates) keep the case loop below
+            if constexpr (!MRP_VEL_BFREE_LANES || Pick::LANES) {
+                // All four cases evaluated at once and the first that holds picked by selects, in Box2D's
+                // order (both points active; point 1 only; point 2 only; none), so no case test waits on
+                // the one before it.  The launches' slowest lanes mostly run the later cases (v0: 72 %
+                // of their 2-point updates, v2: all; oracle b2o_lcp_cases on the captured lane-steps),
+                // which the case-by-case branches reach only after one to three failed tests.
+                const float x2 = -c.nmass0 * b.x, v2 = c.k01.y * x2 + b.y;   // case 2: x = (x2, 0), vn2 = k1 x2 + b.y
+                const float x3 = -c.nmass1 * b.y, v3 = c.k01.y * x3 + b.x;   // case 3: x = (0, x3), vn1 = k1 x3 + b.x
+                const bool c1 = x.x >= 0.0f && x.y >= 0.0f, c2 = x2 >= 0.0f && v2 >= 0.0f, c3 = x3 >= 0.0f && v3 >= 0.0f;
+                P2 xs;
+                xs.x = c1 ? x.x : (c2 ? x2 : 0.0f);
+                xs.y = c1 ? x.y : (c2 ? 0.0f : (c3 ? x3 : 0.0f));
 #if MRP_VEL_BFREE >= 2
-            // whether any case holds picked per lane as well: the impulse is applied unconditionally and
-            // each output selected between the applied and the incoming value (the same bits either
-            // way), so no ballot -> scalar -> branch sits on the chain.  Every lane decides from its
-            // own values, which is the decision the kept lane needs (PickUni: identical lanes;
-            // PickLane: lane i keeps contact i's own result)
-            const bool any = c1 || c2 || c3 || (b.x >= 0.0f && b.y >= 0.0f);
-            const P2 vA0 = vA, vB0 = vB, ni0 = ni;
-            const float wA0 = wA, wB0 = wB;
-            apply(xs);
-            vA.x = any ? vA.x : vA0.x; vA.y = any ? vA.y : vA0.y; wA = any ? wA : wA0;
-            vB.x = any ? vB.x : vB0.x; vB.y = any ? vB.y : vB0.y; wB = any ? wB : wB0;
-            ni.x = any ? ni.x : ni0.x; ni.y = any ? ni.y : ni0.y;
-            (void)pick;
+                // whether any case holds picked per lane as well: the impulse is applied unconditionally and
+                // each output selected between the applied and the incoming value (the same bits either
+                // way), so no ballot -> scalar -> branch sits on the chain.  Every lane decides from its
+                // own values, which is the decision the kept lane needs (PickUni: identical lanes;
+                // PickLane: lane i keeps contact i's own result)
+                const bool any = c1 || c2 || c3 || (b.x >= 0.0f && b.y >= 0.0f);
+                const P2 vA0 = vA, vB0 = vB, ni0 = ni;
+                const float wA0 = wA, wB0 = wB;
+                apply(xs);
+                vA.x = any ? vA.x : vA0.x; vA.y = any ? vA.y : vA0.y; wA = any ? wA : wA0;
+                vB.x = any ? vB.x : vB0.x; vB.y = any ? vB.y : vB0.y; wB = any ? wB : wB0;
+                ni.x = any ? ni.x : ni0.x; ni.y = any ? ni.y : ni0.y;
+                (void)pick;
 #else
-            // some case holds (else Box2D gives up and leaves the contact unchanged): one ballot per compare
-            const uint64_t ok = (__builtin_amdgcn_ballot_w64(x.x >= 0.0f) & __builtin_amdgcn_ballot_w64(x.y >= 0.0f)) |
-                                (__builtin_amdgcn_ballot_w64(x2 >= 0.0f) & __builtin_amdgcn_ballot_w64(v2 >= 0.0f)) |
-                                (__builtin_amdgcn_ballot_w64(x3 >= 0.0f) & __builtin_amdgcn_ballot_w64(v3 >= 0.0f)) |
-                                (__builtin_amdgcn_ballot_w64(b.x >= 0.0f) & __builtin_amdgcn_ballot_w64(b.y >= 0.0f));
-            if (pick.mask(ok)) apply(xs);
+                // some case holds (else Box2D gives up and leaves the contact unchanged): one ballot per compare
+                const uint64_t ok = (__builtin_amdgcn_ballot_w64(x.x >= 0.0f) & __builtin_amdgcn_ballot_w64(x.y >= 0.0f)) |
+                                    (__builtin_amdgcn_ballot_w64(x2 >= 0.0f) & __builtin_amdgcn_ballot_w64(v2 >= 0.0f)) |
+                                    (__builtin_amdgcn_ballot_w64(x3 >= 0.0f) & __builtin_amdgcn_ballot_w64(v3 >= 0.0f)) |
+                                    (__builtin_amdgcn_ballot_w64(b.x >= 0.0f) & __builtin_amdgcn_ballot_w64(b.y >= 0.0f));
+                if (pick.mask(ok)) apply(xs);
 #endif
+            } else {
+                bool ok = true;
+                if (MRP_UNLIKELY(!pick.both(x.x >= 0.0f, x.y >= 0.0f))) {
+                    x.x = -c.nmass0 * b.x; x.y = 0.0f;
+                    vn2 = c.k01.y * x.x + b.y;
+                    if (!pick.both(x.x >= 0.0f, vn2 >= 0.0f)) {
+                        x.x = 0.0f; x.y = -c.nmass1 * b.y;
+                        vn1 = c.k01.y * x.y + b.x;
+                        if (!pick.both(x.y >= 0.0f, vn1 >= 0.0f)) {
+                            x.x = 0.0f; x.y = 0.0f;
+                            ok = pick.both(b.x >= 0.0f, b.y >= 0.0f);
+                        }
+                    }
+                }
+                if (ok) apply(x);
+            }
 #elif MRP_VEL_SPEC
             // case 1 (both points active) applied speculatively, its test resolved after the
             // application: the branch leaves the dependency chain.  When case 1 does not hold, the
