@@ -67,9 +67,13 @@ _FRESH = ["-DMRP_FRESH_REGS=1"]
 # branch-free selection): slowest lane-steps +1.4 %, driver window +1.2 %, steps 21-220 +0.1 %, a
 # whole episode -1.0 % (profiles/r5_ab_v0_pick2_vtcross.txt).
 _PICK2_VT = ["-DMRP_VEL_PICK2=1", "-DMRP_VEL_VTCROSS=1"]
+# ... and the branch-free selection (selects form) on its lanes path only (3+ contacts; the one- and
+# two-contact register paths keep the case loop): slowest lane-steps +1.1 %, driver window +0.8 %,
+# steps 21-220 +0.4 %, whole episode -0.1 % (profiles/r5_ab_v0_bfree_lanes.txt).
+_BFREE_LANES = ["-DMRP_VEL_BFREE=2", "-DMRP_VEL_BFREE_LANES=1"]
 # v3 has the same spill pattern under the iterative-ilp schedule (14 VGPR spills -> 4): PMC traffic
 # 30.8 -> 23.6 MB per launch, slowest lane-steps +0.7 %, driver window level (profiles/r5_ab_v3_fresh.txt).
-UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS + _ITER_ILP + _FRESH + _PICK2_VT, "mrp_env1.hip": _MAX_ILP, "mrp_env2.hip": _GRANULES + _MAX_ILP + _BFREE,
+UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS + _ITER_ILP + _FRESH + _PICK2_VT + _BFREE_LANES, "mrp_env1.hip": _MAX_ILP, "mrp_env2.hip": _GRANULES + _MAX_ILP + _BFREE,
               "mrp_env4.hip": _ILP_LOOPS + _BFREE, "mrp_env5.hip": _LANES_PAIRS + _ITER_ILP + _FRESH}
 # -fno-slp-vectorize: the serial solver chains are latency-bound; packing pairs of f32 ops into
 # v_pk_* costs operand-shuffling moves on the dependency chain (measured +2-3 % env-steps/s off)
