@@ -235,6 +235,10 @@ def main():
                          "with several ranks on one GPU, where RCCL refuses duplicate devices)")
     ap.add_argument("--same-device", action="store_true",
                     help="N>1 rehearsal on one GPU: every rank uses device 0 (with --dist-backend gloo)")
+    ap.add_argument("--force-collective", action="store_true",
+                    help="run the distributed branch (init_process_group, per-step gather) even at WORLD_SIZE 1, so a "
+                         "one-GPU box executes the RCCL gather on device tensors (launch under torch.distributed.run "
+                         "--nproc-per-node 1)")
     ap.add_argument("--dump-gather", default="",
                     help="N>1 check: rank 0 saves every timed step's gathered (obs | reward | done) rows to this .npy")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -257,6 +261,12 @@ def main():
     ap.add_argument("--vecnormalize", action="store_true",
                     help="also run SB3 VecNormalize + Monitor statistics on the device every step (train.py:68,80-82)")
     args = ap.parse_args()
+    if args.same_device and args.dist_backend != "gloo":
+        ap.error("--same-device needs --dist-backend gloo (RCCL refuses two ranks on one device)")
+    if args.same_device and int(os.environ.get("WORLD_SIZE", "1")) < 2:
+        ap.error("--same-device is a rehearsal of N > 1 ranks on one GPU: launch 2+ ranks under torch.distributed.run")
+    if args.force_collective and "WORLD_SIZE" not in os.environ:
+        ap.error("--force-collective: launch under torch.distributed.run (WORLD_SIZE / MASTER_ADDR come from it)")
 
     import torch
     import torch.distributed as dist
@@ -270,7 +280,7 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("for --gpus > 1 launch with torch.distributed.run --nproc-per-node N")
-    distributed = world > 1
+    distributed = world > 1 or args.force_collective
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (libmrp has no CPU fallback)")
     gpu = 0 if args.same_device else local_rank
@@ -301,14 +311,15 @@ def main():
     trunc = torch.zeros(L, dtype=torch.uint8, device=dev)
     status = torch.zeros(L, dtype=torch.uint8, device=dev)
     # one contiguous buffer per rank for the gather: [obs | reward | done] as float32
-    gather = StepGather(Shard(rank, world, L), O, dev, host_stage=host_coll) if distributed and not args.no_gather else None
+    gather = (StepGather(Shard(rank, world, L), O, dev, host_stage=host_coll, force_collective=args.force_collective)
+              if distributed and not args.no_gather else None)
     dumps = [] if (args.dump_gather and rank == 0 and gather is not None) else None
 
     b.reset()   # device-RNG spawns for every lane (seeded by global lane id)
     norm = None
     if args.vecnormalize:
         from gym_puzzles_amd import DeviceVecNormalize
-        norm = DeviceVecNormalize(L, O, local_rank)
+        norm = DeviceVecNormalize(L, O, gpu)
         term = torch.zeros((L, O), dtype=torch.float32, device=dev)
         nobs, nrew, nterm = torch.zeros_like(obs), torch.zeros_like(rew), torch.zeros_like(term)
         epr, epl = torch.zeros(L, dtype=torch.float64, device=dev), torch.zeros(L, dtype=torch.int32, device=dev)
@@ -355,7 +366,10 @@ def main():
         if gather is not None:
             gather(nobs if norm is not None else obs, nrew if norm is not None else rew, done)
             if dumps is not None:
-                dumps.append(gather.full.to("cpu", copy=True))
+                # an asynchronous copy on the stream (device buffer) or a host memcpy (host-staged):
+                # no synchronising device -> host transfer in the timed loop; the JSON line is marked
+                # (config.dump_gather) so its rate is never quoted as throughput
+                dumps.append(gather.full.clone())
     r1.record(stream)
     torch.cuda.synchronize(dev)
     if distributed:
@@ -483,8 +497,11 @@ def main():
             "data": "synthetic: device-RNG random actions, device-RNG spawns (reference draw ranges)",
             "config": {"workload": f"{ENV_NAMES[args.env]}, {L} lanes/GPU, random actions, auto-reset", "env_id": args.env,
                        "lanes_per_gpu": L, "global_lanes": world * L,
-                       "parallelism": f"lane-sharded x{world}" + ("" if world == 1 or args.no_gather else " + gather to rank 0/step"),
-                       "collective": None if world == 1 else (args.dist_backend + (" (host-staged)" if host_coll else " (RCCL)")),
+                       "parallelism": f"lane-sharded x{world}" + ("" if not distributed or args.no_gather else " + gather to rank 0/step"),
+                       "collective": None if not distributed or args.no_gather else
+                                     (args.dist_backend + (" (host-staged)" if host_coll else " (RCCL)")
+                                      + (" forced at world size 1" if world == 1 else "")),
+                       "dump_gather": bool(dumps is not None),
                        "devices": 1 if (world == 1 or args.same_device) else world,
                        "vecnormalize": bool(args.vecnormalize),
                        "dispatch": ("lane order" if args.schedule == 0 else f"mrp_set_schedule({args.schedule})") if args.schedule >= 0
@@ -514,7 +531,7 @@ def main():
             cb["gpu_over_cpu"] = {"port": value / cb["value"], "early_exit_port": value / cb["early_exit_port"]["value"]}
         print(json.dumps(line), flush=True)
     if dumps is not None:
-        np.save(args.dump_gather, torch.stack(dumps).numpy())
+        np.save(args.dump_gather, torch.stack(dumps).cpu().numpy())
     b.close()
     if distributed:
         dist.destroy_process_group()

@@ -132,8 +132,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.mrp_debug_trace_words.argtypes = []
     L.mrp_debug_progress.argtypes = [i, ctypes.POINTER(P), i]
     L.mrp_debug_velbench.argtypes = [i, i, i, i, i, P]
-    if hasattr(L, "mrp_debug_posbench"):   # A/B libraries built before round 5's position micro-benchmark lack it
-        L.mrp_debug_posbench.argtypes = [i, i, i, i, i, P]
+    L.mrp_debug_posbench.argtypes = [i, i, i, i, i, P]
     _lib = L
     return L
 

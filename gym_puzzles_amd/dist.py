@@ -40,12 +40,15 @@ def shard_from_env(lanes_per_rank: int) -> Shard:
 class StepGather:
     """Packs one step's outputs of this rank and gathers every rank's block to rank 0."""
 
-    def __init__(self, shard: Shard, obs_dim: int, device, group=None, to_all: bool = False, host_stage: bool = False):
+    def __init__(self, shard: Shard, obs_dim: int, device, group=None, to_all: bool = False, host_stage: bool = False,
+                 force_collective: bool = False):
         """``host_stage``: the collective runs on host memory (a CPU backend such as gloo): the packed
         block is copied from the device into a pinned host buffer and gathered there; the receive
-        buffer is on the host too."""
+        buffer is on the host too.  ``force_collective``: call the collective at world size 1 too
+        (a one-GPU box then executes the RCCL gather on device tensors; bench.py --force-collective)."""
         import torch
         self.shard, self.obs_dim, self.group, self.to_all = shard, obs_dim, group, to_all
+        self.force_collective = force_collective
         L = shard.lanes_per_rank
         self.packed = torch.zeros((L, obs_dim + 2), dtype=torch.float32, device=device)
         self.host = torch.zeros((L, obs_dim + 2), dtype=torch.float32).pin_memory() if host_stage else None
@@ -71,7 +74,7 @@ class StepGather:
         if self.host is not None:
             self.host.copy_(p)   # synchronous device -> pinned host copy: the CPU collective reads it next
             p = self.host
-        if self.shard.world == 1:
+        if self.shard.world == 1 and not self.force_collective:
             full = p
         else:
             if self.to_all:

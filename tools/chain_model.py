@@ -7,7 +7,7 @@ island's Gauss-Seidel order into dependency levels would remove.
 
 Costs per unit are one wave's measured cycles (~900 cycles per velocity contact update,
 ~850 per position point update incl. its b2Rot::Set, ~25 K per TOI event, ~60 K of fixed per-step
-work).  With a kernel trace of bench.py (tools/r3_session.sh) the model is set beside the measured
+work).  With a kernel trace of bench.py (tools/sessions/r3_session.sh) the model is set beside the measured
 per-launch durations of the same steps.
 """
 from __future__ import annotations

@@ -2,7 +2,7 @@
 
     python tools/issue_roofline.py DIR OUT.json [ENV ...]
 
-For each config, DIR holds (tools/r4_session2.sh): cap_env<E>.npz (the 20 slowest lane-steps of the
+For each config, DIR holds (tools/sessions/r4_session2.sh): cap_env<E>.npz (the 20 slowest lane-steps of the
 driver window with their in-batch phase traces), replay_stamps_env<E>.json (the same lane-steps
 stepped alone by the stamps library), pmc_env<E>/ (rocprofv3 SQ_INSTS_* counters of each lone
 replay: exactly that lane-step's executed instructions) and kt_env<E>/ (their lone-wave durations).

@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ instruction counters of the micro-benchmarks and of the chain replays (one library):
-#   tools/r5_pmc.sh OUTDIR [LIB]
+#   tools/pmc_micro.sh OUTDIR [LIB]
 # One rocprofv3 --pmc pass per program, under its own time limit; stops at the first failure.
 set -uo pipefail
 OUT=gpurun_out/$1; LIB=${2:-gym_puzzles_amd/libmrp.so}

@@ -4,7 +4,7 @@
 # rocprofv3 set of every config over the same window (kernel trace, FETCH_SIZE, WRITE_SIZE; VALU
 # counters for v0), then the default and driver-window v0 lines with every diagnostic.
 # Local half: WARMUP=5 STEPS=20 tools/collect_profiles.sh <tag>.  The chain stops at the first failure.
-#   tools/r3_final.sh [tag]   (default r3f)
+#   tools/sessions/r3_final.sh [tag]   (default r3f)
 set -uo pipefail
 TAG=${1:-r3f}
 mkdir -p gpurun_out

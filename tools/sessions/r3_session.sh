@@ -3,7 +3,7 @@
 # baseline, as the driver runs it), the default bench line, and a kernel-trace profile of the
 # driver window (its per-launch k_step average over exactly the timed launches).  Each GPU step
 # has its own time limit; the chain stops at the first failure.
-#   tools/r3_session.sh <tag> [skip-tests]
+#   tools/sessions/r3_session.sh <tag> [skip-tests]
 set -uo pipefail
 TAG=${1:-r3}
 mkdir -p gpurun_out

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 final evidence, second call: the rocprofv3 set of every BASELINE config over the driver
 # window (kernel trace + stats, FETCH_SIZE, WRITE_SIZE in separate passes; tools/profile.sh), then
-# the issue-count roofline inputs (tools/r4_session2.sh's capture / replay with the atomic-free
+# the issue-count roofline inputs (tools/sessions/r4_session2.sh's capture / replay with the atomic-free
 # stamps build): the launches' slowest lane-steps captured in the batch, replayed alone under the
 # SQ_INSTS counters and the kernel trace.  Local half: tools/collect_profiles.sh r4f and
 # tools/issue_roofline.py gpurun_out/r4f2 profiles/r4_issue_roofline.json.

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-5 GPU session: [GPU suite] + chain bench (the launches' slowest lane-steps replayed alone)
 # + velbench + driver-window bench, for the default library and optional variant libraries.
-#   tools/r5_session.sh OUTDIR "TESTS(0/1)" "LIB1.so LIB2.so ..." [ENVS] [BENCH(0/1)]
+#   tools/sessions/r5_session.sh OUTDIR "TESTS(0/1)" "LIB1.so LIB2.so ..." [ENVS] [BENCH(0/1)]
 # Every GPU step has its own time limit; the chain stops at the first failure.
 set -uo pipefail
 OUT=gpurun_out/$1; TESTS=$2; LIBS=$3; ENVS=${4:-0,1,2,4,5}; BENCH=${5:-1}

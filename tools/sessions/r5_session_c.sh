@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 timeout -k 10 400 python -u tools/chain_bench.py $O/chain.json --envs 0 --repeat 5 --rounds 2 \
     --libs gym_puzzles_amd/libmrp.so,gym_puzzles_amd/var/v5.so > $O/chain.txt 2>&1 || { echo "chain failed"; tail $O/chain.txt; exit 1; }
 tail -3 $O/chain.txt
-bash tools/r5_windows.sh r5sc "gym_puzzles_amd/libmrp.so gym_puzzles_amd/var/v5.so" || exit 1
+bash tools/windows_ab.sh r5sc "gym_puzzles_amd/libmrp.so gym_puzzles_amd/var/v5.so" || exit 1
 STEPS=20 WARMUP=5 LANES=1024 timeout -k 10 400 bash tools/profile.sh r5_v2 2 > /dev/null || { echo "profile 2 failed"; exit 1; }
 STEPS=20 WARMUP=5 LANES=1024 timeout -k 10 400 bash tools/profile.sh r5_heavy_v2_3block 4 > /dev/null || { echo "profile 4 failed"; exit 1; }
 echo profiles done

@@ -10,7 +10,7 @@ mkdir -p $O
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 export TMPDIR=/tmp
-bash tools/r5_windows_args.sh r5sg "base=gym_puzzles_amd/libmrp.so" "base_s2=gym_puzzles_amd/libmrp.so:--schedule,2" \
+bash tools/windows_ab_args.sh r5sg "base=gym_puzzles_amd/libmrp.so" "base_s2=gym_puzzles_amd/libmrp.so:--schedule,2" \
     "xg_s2=gym_puzzles_amd/var/xg.so:--schedule,2" || exit 1
 EXTRA="--schedule 2" bash tools/traffic_ab.sh gym_puzzles_amd/var/xg.so > $O/traffic_xg.txt 2>&1 || { echo "traffic xg failed"; exit 1; }
 tail -1 $O/traffic_xg.txt | cut -c1-200

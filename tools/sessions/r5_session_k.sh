@@ -16,7 +16,7 @@ for lib in gym_puzzles_amd/libmrp.so gym_puzzles_amd/var/bf2.so; do
   MRP_LIB=$lib timeout -k 10 120 python -u tools/velbench.py > "$O/velbench_$(basename $lib .so).txt" 2>&1 || { echo "velbench failed"; exit 1; }
   grep "blocks     1" "$O/velbench_$(basename $lib .so).txt" | sed "s/^/$(basename $lib .so): /"
 done
-bash tools/r5_windows.sh r5sk "gym_puzzles_amd/libmrp.so gym_puzzles_amd/var/bf2.so" || exit 1
+bash tools/windows_ab.sh r5sk "gym_puzzles_amd/libmrp.so gym_puzzles_amd/var/bf2.so" || exit 1
 for r in 0 1; do for e in 2 4; do for lib in gym_puzzles_amd/libmrp.so gym_puzzles_amd/var/bf2.so; do
   MRP_LIB=$lib timeout -k 10 200 python bench.py --env $e --lanes 1024 --steps 20 --warmup 5 --no-cpu-baseline --single-env 0 --later-window 0 --episode 0 --multi-step 0 \
       > $O/drv${e}_$(basename $lib .so)_$r.log 2>&1 || { echo "bench failed"; exit 1; }

@@ -16,5 +16,5 @@ for lib in gym_puzzles_amd/libmrp.so gym_puzzles_amd/var/bfl.so; do
   MRP_LIB=$lib timeout -k 10 120 python -u tools/velbench.py > "$O/velbench_$(basename $lib .so).txt" 2>&1 || { echo "velbench failed"; exit 1; }
   grep "blocks     1" "$O/velbench_$(basename $lib .so).txt" | sed "s/^/$(basename $lib .so): /"
 done
-bash tools/r5_windows.sh r5sn "gym_puzzles_amd/libmrp.so gym_puzzles_amd/var/bfl.so" || exit 1
+bash tools/windows_ab.sh r5sn "gym_puzzles_amd/libmrp.so gym_puzzles_amd/var/bfl.so" || exit 1
 exit 0

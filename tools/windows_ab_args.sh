@@ -1,6 +1,6 @@
 #!/bin/bash
 # v0 bench windows for library + bench-argument variants, interleaved over two rounds (GPU box):
-#   tools/r5_windows_args.sh OUTDIR "name=LIB.so[:extra bench args with , for spaces]" ...
+#   tools/windows_ab_args.sh OUTDIR "name=LIB.so[:extra bench args with , for spaces]" ...
 # driver window (steps 6-25), bench default (steps 21-220) and one whole episode per entry; each
 # run under its own time limit, the first failure ends the script.
 set -uo pipefail
