@@ -136,27 +136,45 @@ def cpu_baseline(env_id: int, lanes: int, seed: int, skip: int, steps: int, epis
     return out
 
 
-def single_env_rate(env_id: int, steps: int = 300) -> dict:
+def single_env_rate(env_id: int, steps: int = 300, seeds=(0, 1, 2, 3)) -> dict:
     """Diagnostic (never `value`): the gym-style drop-in path, `make(id)` then env.step(a) with host
-    numpy actions - one lane per call, PCIe round trip included (what train.py's DummyVecEnv drives)."""
+    numpy actions - one lane per call, PCIe round trip included (what train.py's DummyVecEnv drives).
+
+    The step is one 1-lane k_step launch, i.e. one lane's serial chain, so its time follows the
+    episode: an agent pressed against the block runs the 180 velocity sweeps and the position passes,
+    a free one does not.  The reference's reset draws its spawn from the global np.random, which an
+    unseeded run leaves at a random state, and that made single runs bimodal (36-39 us against
+    48-61 us in round 5).  Each timed episode here starts from np.random.seed(s) for the listed seeds
+    (the same spawn and actions every run), and the line reports their mean with the per-seed times
+    and the lane's touching contacts and position iterations per step."""
     from gym_puzzles_amd import make
     name, kw = SINGLE_ENV_MAKE[env_id]
-    env = make(name, **kw)
-    env.reset()
-    rs = np.random.RandomState(0)
-    acts = rs.uniform(-1, 1, size=(steps + 20, env.action_space.shape[0])).astype(np.float32)
-    for k in range(20):
-        _, _, d, _ = env.step(acts[k])
-        if d:
-            env.reset()
-    t0 = time.perf_counter()
-    for k in range(steps):
-        _, _, d, _ = env.step(acts[20 + k])
-        if d:
-            env.reset()
-    dt = time.perf_counter() - t0
-    env.close()
-    return {"env_steps_per_s": steps / dt, "us_per_step": dt / steps * 1e6, "steps": steps,
+    per = []
+    for sd in seeds:
+        np.random.seed(sd)   # the reference's spawn RNG (global np.random, SURVEY Appendix C.2)
+        env = make(name, **kw)
+        env.unwrapped.seed(sd)
+        env.reset()
+        rs = np.random.RandomState(sd)
+        acts = rs.uniform(-1, 1, size=(steps + 20, env.action_space.shape[0])).astype(np.float32)
+        for k in range(20):
+            _, _, d, _ = env.step(acts[k])
+            if d:
+                env.reset()
+        c0 = env.unwrapped._b.counters_ex()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            _, _, d, _ = env.step(acts[20 + k])
+            if d:
+                env.reset()
+        dt = time.perf_counter() - t0
+        c1 = env.unwrapped._b.counters_ex()
+        env.close()
+        per.append({"seed": sd, "us_per_step": dt / steps * 1e6,
+                    "touching_contacts_per_step": (c1["touching_contacts"] - c0["touching_contacts"]) / steps,
+                    "position_iterations_per_step": (c1["position_iterations"] - c0["position_iterations"]) / steps})
+    us = float(np.mean([p["us_per_step"] for p in per]))
+    return {"env_steps_per_s": 1e6 / us, "us_per_step": us, "steps": steps, "seeds": list(seeds), "per_seed": per,
             "path": f"gym_puzzles_amd.make('{name}'{''.join(f', {k}={v!r}' for k, v in kw.items())}).step(): "
                     "1-lane kernel, actions and outputs through the ctx's pinned host buffer"}
 

@@ -14,6 +14,7 @@ import math
 import random
 import struct
 
+import numpy as np
 import pytest
 
 FLT_MAX = 3.4028234663852886e38
@@ -203,3 +204,32 @@ def test_dual_schedule_keeps_every_body_in_sequential_order():
                         got[b].append(i)
         assert n_upd == nc * D and sweeps_run == [D] * nc
         assert got == seq
+
+
+def test_one_rot_fixed_angle_stays_positive_zero():
+    """The position passes' ONE_ROT rotations (mrp_world.h one_rot): a body with invI = 0 whose angle
+    is +0 keeps the bit pattern +0 through every point update (a - 0 * x and a + 0 * x, float32), for
+    every finite x, so its rotation is b2Rot::Set(+0) = {+0, 1}; an infinite or NaN x makes it NaN,
+    which the pass check sends back to the memo path."""
+    rs = np.random.RandomState(3)
+    bits = np.r_[rs.randint(0, 2 ** 32, 200000, dtype=np.uint64).astype(np.uint32),
+                 np.array([0, 0x80000000, 1, 0x80000001, 0x7f7fffff, 0xff7fffff, 0x00800000, 0x80800000], np.uint32)]
+    x = bits.view(np.float32)
+    zero, izero = np.float32(0.0), np.float32(0.0)   # the angle +0 and invI = +0
+    with np.errstate(invalid="ignore", over="ignore"):
+        sub = zero - izero * x     # aA -= iA * cross(rA, P)
+        add = zero + izero * x     # aB += iB * cross(rB, P)
+    fin = np.isfinite(x)
+    assert (sub[fin].view(np.uint32) == 0).all() and (add[fin].view(np.uint32) == 0).all()
+    assert np.isnan(sub[~fin]).all() and np.isnan(add[~fin]).all()
+
+
+def test_rot_fast_end_is_glibc_branch_point():
+    """ROT_FAST_END (0x42f00000, the bits of 120.0f): rot() takes rot_fast exactly when
+    abstop12(y) < abstop12(120.0f), i.e. when the |y| bit pattern is below ROT_FAST_END (NaN and
+    infinities above it)."""
+    assert int(np.float32(120.0).view(np.uint32)) == 0x42F00000
+    rs = np.random.RandomState(5)
+    b = rs.randint(0, 2 ** 32, 500000, dtype=np.uint64).astype(np.uint32)
+    abstop12 = (b >> 20) & 0x7FF
+    assert np.array_equal(abstop12 < 0x42F, (b & 0x7FFFFFFF) < 0x42F00000)
