@@ -345,3 +345,39 @@ def test_v2_update_params_formula():
                        (2.14, 0.7), 3.0, 0.97)
     assert (r.shaped_bounds_penalty, r.shaped_blk_bounds_penalty, r.shaped_puzzle_reward) == (e_pen, e_blk, e_puz)
     assert math.isclose(r.shaped_bounds_penalty, 1095.6, rel_tol=1e-3)
+
+
+def test_distance_pow_semantics_known_case(orc):
+    """The device takes Python's `(a - b) ** 2` as a multiply and `** 0.5` as sqrt (mrp_env.h
+    py_distance); the reference's CPython calls glibc pow for both (<= 0.52 ulp, not correctly
+    rounded), and so does the oracle.  The two differ in the last bit of the float64 distance for rare
+    inputs.  This pins the divergence on the rollouts that found it (envs 2 / 3 / 8, seed 11): every
+    differing distance is 1 ulp apart, its float32 rounding (what the observation stores) is the same
+    under both, and the float64 reward moves by far less than tests/test_gpu.py's 1e-12 tolerance."""
+    def dist_device(p, q):   # x * x and a correctly rounded sqrt, as py_distance
+        dx, dy = p[0] - q[0], p[1] - q[1]
+        return math.sqrt(dx * dx + dy * dy)
+    found = 0
+    for env_id in (2, 3, 8):
+        e = orc.OracleEnv(env_id)
+        rs = np.random.RandomState(11)
+        draws = reference_draws(env_id, rs)
+        acts = rs.uniform(-1, 1, (80, e.act_dim)).astype(np.float32)
+        e.reset(np.asarray(draws, np.float64), np.zeros(e.act_dim, np.float32))
+        r = _Restated(e, (draws[-2], draws[-1]), 3.0, 0.97)
+        e.set_shaped(r.shaped_bounds_penalty, r.shaped_blk_bounds_penalty, r.shaped_puzzle_reward)
+        for a in acts:
+            _, _, done, _ = e.step(a)
+            b = e.bodies().reshape(-1, 6)
+            blk = norm_units((float(b[0, 0]), float(b[0, 1])))
+            pairs = [(blk, r.goal[:2])] + [(norm_units((float(b[1 + i, 0]), float(b[1 + i, 1]))), blk) for i in range(r.na)]
+            for p, q in pairs:
+                ref, dev = distance(p, q), dist_device(p, q)
+                if ref != dev:
+                    found += 1
+                    assert abs(np.float64(ref).view(np.int64) - np.float64(dev).view(np.int64)) == 1
+                    assert np.float32(ref) == np.float32(dev)
+                    assert abs(ref - dev) * 25.0 < 1e-12 * max(1.0, abs(ref))   # the largest reward weight
+            if done:
+                break
+    assert found >= 1, "the known pow / multiply divergence of these rollouts disappeared"

@@ -5,8 +5,8 @@ untouched, so experiment arms never enter the shipped headers):
     MRP_VARIANT_WORKTREE=1 python tools/patch_variant.py ...           (base: the working tree)
 
 SPEC.py defines EDITS = [(file, old, new), ...] (exact text replacements, each `old` must occur
-in the file) and optionally FLAGS = {"mrp_envE.hip": [...]} (that unit's compile flags instead of
-build.py's UNIT_FLAGS entry).  Only the listed env units are compiled from the patched copy; the other
+in the file), optionally FLAGS = {"mrp_envE.hip": [...]} (that unit's compile flags instead of
+build.py's UNIT_FLAGS entry) and DEFINES = ["NAME", ...] (-D for every unit, e.g. MRP_STAMPS).  Only the listed env units are compiled from the patched copy; the other
 units are the default library's objects (python -m gym_puzzles_amd.build first).  Every edit must keep
 the LaneState / EnvOps layout (mrp_create checks each unit's compiled dims).
 """
@@ -52,7 +52,7 @@ def main():
     B.DEPS = B.SOURCES + [os.path.join(csrc, os.path.basename(x)) for x in B.DEPS if x.endswith(".h")]
     B.UNIT_FLAGS = dict(B.UNIT_FLAGS, **s.get("FLAGS", {}))
     os.environ["MRP_ALLOW_STALE_UNITS"] = "1"
-    print(B.build(verbose=True, out=out, only_envs=envs))
+    print(B.build(verbose=True, out=out, only_envs=envs, defines=tuple(s.get("DEFINES", ()))))
 
 
 if __name__ == "__main__":

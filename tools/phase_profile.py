@@ -24,6 +24,9 @@ NAMES = ["load+act", "apply_actions", "FNC(new fixtures)", "collide", "solve(isl
 # updates run, 16 velocity-sweep cycles, 17 position-pass cycles, 18 island set-up cycles (thread 0),
 # 19 largest island's contact count, 20/21 TOI split (scan + b2TimeOfImpact, events), 22/23 collide split (narrow phase, commit)
 SUB = {"velocity_sweeps": 16, "position_passes": 17, "island_setup": 18}
+# round 6 (trace rows of 40 words): the solve's thread-0 bookkeeping and the TOI scan alone
+SUB2 = {"island_building": 32, "island_writeback_integrate": 33, "fixture_sync": 34}
+TOI_SCAN = 35
 
 
 def main():
@@ -67,6 +70,9 @@ def main():
                "total_us_mean": float(slow[:, 11].mean() / ghz / 1e3),
                "phases_cycles_mean": {n: float(slow[:, i].mean()) for i, n in enumerate(NAMES)},
                "solve_split_cycles_mean": {k: float(slow[:, w].mean()) for k, w in SUB.items()},
+               "solve_bookkeeping_cycles_mean": ({k: float(slow[:, w].mean()) for k, w in SUB2.items()}
+                                                 if slow.shape[1] > 35 else None),
+               "toi_scan_alone_cycles_mean": float(slow[:, TOI_SCAN].mean()) if slow.shape[1] > 35 else None,
                "island_contacts_mean": float(slow[:, 12].mean()), "toi_events_mean": float(slow[:, 13].mean()),
                "position_passes_mean": float(slow[:, 14].mean()), "velocity_updates_mean": float(slow[:, 15].mean()),
                "largest_island_contacts_mean": float(slow[:, 19].mean()),
@@ -88,8 +94,12 @@ def main():
         print(f"  {n:20s} {res['mean_lane_step_phases'][n]:10.0f} {v:10.0f} {100 * v / s['total_cycles_mean']:5.1f}%")
     for k, v in s["solve_split_cycles_mean"].items():
         print(f"    solve: {k:16s} {v:10.0f} {100 * v / s['total_cycles_mean']:5.1f}%")
+    if s["solve_bookkeeping_cycles_mean"]:
+        for k, v in s["solve_bookkeeping_cycles_mean"].items():
+            print(f"    solve: {k:16s} {v:10.0f} {100 * v / s['total_cycles_mean']:5.1f}%")
     t = s["toi_split_cycles_mean"]
-    print(f"    TOI: scan + b2TimeOfImpact {t['scan_and_time_of_impact']:10.0f}, events {t['events']:10.0f}")
+    print(f"    TOI: scan + b2TimeOfImpact {t['scan_and_time_of_impact']:10.0f} (scan alone {s['toi_scan_alone_cycles_mean'] or 0:.0f}), "
+          f"events {t['events']:10.0f}")
     c = s["collide_split_cycles_mean"]
     print(f"    collide: narrow phase {c['narrow_phase']:10.0f}, serial commit {c['serial_commit']:10.0f}")
     print(f"  slowest lane: island contacts {s['island_contacts_mean']:.2f}, velocity updates {s['velocity_updates_mean']:.0f}, "
