@@ -53,27 +53,27 @@ _ITER_ILP = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
 # a cross product): their slowest lane-steps replayed alone +0.8 % / +3.3 %, bitwise; v0 -0.1 % (the
 # selects and ballots add to every two-point update what the saved case tests take off), so v0 keeps
 # the case loop; Heavy-v0 -1.0 % and v3 -4.9 % (profiles/r5_ab_bfree_env1_env5.txt) keep it too.
-# With the "any case holds" test as per-lane selects as well (-DMRP_VEL_BFREE=2: the impulse applied
+# With the "any case holds" test as per-lane selects as well (round 5's MRP_VEL_BFREE=2: the impulse applied
 # unconditionally, each output selected, no ballot -> branch on the chain): v2 +2.8 % / +2.5 %,
 # 3-block +2.4 % / +2.6 % (slowest lane-steps / driver window) over the ballot form; v0 +1.1 % in the
 # driver window but -5 % over a whole episode (profiles/r5_ab_bfree2.txt), so v0 keeps the case loop.
-_BFREE = ["-DMRP_VEL_BFREE=2", "-DMRP_VEL_PICK2=1", "-DMRP_VEL_VTCROSS=1"]
+_BFREE = ["-DMRP_VEL_BFREE=1", "-DMRP_VEL_PICK2=1", "-DMRP_VEL_VTCROSS=1"]
 # v0 makes the values its step needs late (the state store's per-thread offsets, the TOI phase's
 # zeroes) where they are used (-DMRP_FRESH_REGS=1): VGPR spills 14 -> 4, scratch 48 -> 16 B per
 # thread, PMC traffic 30.9 -> 23.2 MB per launch; driver window -0.4 %, steps 21-220 -0.2 %, whole
 # episode +0.7 % (profiles/r5_windows_traffic_fresh.txt).
 _FRESH = ["-DMRP_FRESH_REGS=1"]
-# v0 also takes the two-ballot case test and the cross-product tangent speed (without the
-# branch-free selection): slowest lane-steps +1.4 %, driver window +1.2 %, steps 21-220 +0.1 %, a
-# whole episode -1.0 % (profiles/r5_ab_v0_pick2_vtcross.txt).
-_PICK2_VT = ["-DMRP_VEL_PICK2=1", "-DMRP_VEL_VTCROSS=1"]
-# ... and the branch-free selection (selects form) on its lanes path only (3+ contacts; the one- and
-# two-contact register paths keep the case loop): slowest lane-steps +1.1 %, driver window +0.8 %,
-# steps 21-220 +0.4 %, whole episode -0.1 % (profiles/r5_ab_v0_bfree_lanes.txt).
-_BFREE_LANES = ["-DMRP_VEL_BFREE=2", "-DMRP_VEL_BFREE_LANES=1"]
+# v0 takes the branch-free selection (selects form) on its lanes path only (3+ contacts; the one- and
+# two-contact register paths keep the case loop).  Round 6 re-measured it and round 5's two-ballot case
+# test + cross-product tangent speed (MRP_VEL_PICK2 / MRP_VEL_VTCROSS) on all four windows, interleaved
+# on one box (profiles/r6_windows_ab_v0.txt; driver window / steps 21-220 / 501-700 / whole episode
+# against round 5's library): without PICK2_VT +0.9 / +0.7 / +0.7 / +1.3 %, without BFREE_LANES
+# -0.6 / -0.4 / -0.1 / +0.1 %, without both -1.8 / -0.5 / +1.2 / +1.1 %.  So v0 keeps BFREE_LANES and
+# drops PICK2_VT (it bought the driver window with the whole episode, DESIGN.md's rule).
+_BFREE_LANES = ["-DMRP_VEL_BFREE=1", "-DMRP_VEL_BFREE_LANES=1"]
 # v3 has the same spill pattern under the iterative-ilp schedule (14 VGPR spills -> 4): PMC traffic
 # 30.8 -> 23.6 MB per launch, slowest lane-steps +0.7 %, driver window level (profiles/r5_ab_v3_fresh.txt).
-UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS + _ITER_ILP + _FRESH + _PICK2_VT + _BFREE_LANES, "mrp_env1.hip": _MAX_ILP, "mrp_env2.hip": _GRANULES + _MAX_ILP + _BFREE,
+UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS + _ITER_ILP + _FRESH + _BFREE_LANES, "mrp_env1.hip": _MAX_ILP, "mrp_env2.hip": _GRANULES + _MAX_ILP + _BFREE,
               "mrp_env4.hip": _ILP_LOOPS + _BFREE, "mrp_env5.hip": _LANES_PAIRS + _ITER_ILP + _FRESH}
 # -fno-slp-vectorize: the serial solver chains are latency-bound; packing pairs of f32 ops into
 # v_pk_* costs operand-shuffling moves on the dependency chain (measured +2-3 % env-steps/s off)

@@ -712,7 +712,7 @@ __global__ __launch_bounds__(BLOCK, MRP_STEP_WAVES_PER_EU) void k_posbench(int n
     __syncthreads();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     int n = w.solver_position_small(is, sh.u.sol.vcs, sh.u.sol.pcs, false, -1, -1, iters);
-    if (n < 0) n = w.template solver_position_lanes<false>(is, sh.u.sol.vcs, sh.u.sol.pcs, false, -1, -1, iters);
+    if (n < 0) n = w.solver_position_lanes(is, sh.u.sol.vcs, sh.u.sol.pcs, false, -1, -1, iters);
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     __syncthreads();
     if (tid == 0) { out[2 * blockIdx.x] = t1 - t0 + (is.pcx[0] == 12345.0f ? 1ull : 0ull); out[2 * blockIdx.x + 1] = (unsigned long long)n; }

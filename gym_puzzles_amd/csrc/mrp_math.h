@@ -250,11 +250,23 @@ MRP_HD Rot rot_slow(float y) {
     return q;
 }
 
-// the entry point: the fast form below 120 rad, glibc's other branches (Payne-Hanek reduction,
-// inf/nan) out of the common path
+// the entry point.  On the device: the fast form, straight-line, for every input; glibc's other
+// branches (Payne-Hanek reduction at 120 rad and above, inf / NaN) replace its result on the lanes
+// that need them, behind one wave-uniform test that is almost never taken (same bits; the branch in
+// front of the fast form cost a chained call 338 cycles against 226, tools/micro/f64lat.hip; slowest
+// lane-steps alone 1.5 % shorter in v0 / Heavy-v0 / v2, profiles/r6_rot_late_ab.txt)
 MRP_HD Rot rot(float y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    Rot q = rot_fast(y);   // v_cvt_i32_f64 clamps the reduction of |y| >= 120; rot_slow replaces those
+    const bool big = !(abstop12(y) < abstop12(120.0f));
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(big) != 0, 0)) {
+        if (big) q = rot_slow(y);
+    }
+    return q;
+#else
     if (abstop12(y) < abstop12(120.0f)) return rot_fast(y);
     return rot_slow(y);
+#endif
 }
 
 // b2Rot::Set(+-0) = {+-0, 1} exactly (glibc's sinf / cosf return y and 1 below 2^-12): when no

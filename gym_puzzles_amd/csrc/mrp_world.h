@@ -10,9 +10,9 @@
 // lane's persistent state (LaneState<ENV>, a POD of 32-bit words) is stored lane-major in HBM --
 // each lane one contiguous block, moved by the wave as coalesced 16-B granules (mrp_lane.h
 // StateIO) -- and lives in LDS (Shared<ENV>) for the step.  Thread 0 runs the order-sensitive
-// serial parts (tree updates, sorted AddPair, contact commit and events, island DFS and set-up,
-// TOI bookkeeping); all 64 threads run the data-parallel parts (pair tests, one contact's SAT per
-// thread, TOI candidate scans, state I/O); the velocity and position iterations run on the whole
+// serial parts (tree reinsertions, sorted AddPair, contact commit and events, island set-up, TOI
+// bookkeeping); all 64 threads run the data-parallel parts (pair tests, one contact's SAT per
+// thread, the island DFS, the fixtures' swept AABBs, TOI candidate scans, state I/O); the velocity and position iterations run on the whole
 // wave with the island in registers (one or two contacts: every thread evaluates the same update)
 // or spread across the wave (larger islands: contact i's constants in thread i, body k's state in
 // thread k, one contact update after the other through v_readlane / v_writelane).
@@ -32,50 +32,34 @@ namespace mrp {
 
 constexpr int NULLN = -1;
 
-// The solver's sweep / pass loops (one call per island solve).  MRP_SOLVE_NOINLINE (A/B) keeps each
-// as a function of its own, so the machine scheduler treats its loop as it does in a small kernel.
-#ifdef MRP_SOLVE_NOINLINE
-#define MRP_SOLVE_FN __device__ __attribute__((noinline))
-#else
+// MRP_SOLVE_NOINLINE_LANES (build.py: the 3-block unit): the lanes-path sweep / pass loops as functions
+// of their own (one call per island solve), so the machine scheduler treats each loop as it does in a
+// small kernel (profiles/r3g_ab_scheduler.txt).  Every other loop is inlined into k_step.
 #define MRP_SOLVE_FN __device__ __forceinline__
-#endif
 #ifdef MRP_SOLVE_NOINLINE_LANES
 #define MRP_LANES_FN __device__ __attribute__((noinline))
 #else
 #define MRP_LANES_FN MRP_SOLVE_FN
 #endif
-// MRP_SOLVE_NOINLINE_MAIN (A/B): only the main island solve's lanes-path loops out of line (the TOI
-// sub-step solves keep them inlined)
-// The two-body register paths of 3-4 contact islands (sweep_xw / pos_xw) hold three or four contacts'
-// constants in VGPRs; inlined into k_step they pushed its VGPR spills from 9 to 85.  As functions of
-// their own they get the register file to themselves (k_step saves its live registers around the one
-// call per island solve, not per sweep).  MRP_XW_INLINE (A/B) inlines them.
-// MRP_COLLIDE_GROUPS (default 1): the narrow phase of up to 32 contacts on groups of 8 / 4 / 2 lanes
-// per contact (round 4 A/B, profiles/r4_ab_collide_groups.txt: v2 +4.3 %, v3 +0.6 / +1.7 %, v0 +0.2 / +0.9 %)
-#ifndef MRP_COLLIDE_GROUPS
-#define MRP_COLLIDE_GROUPS 1
-#endif
-// MRP_LANES_PAIRS=1: the lanes-path sweeps two per loop trip (lanes_sweeps; build.py sets it for the
-// v0 and v3 units, where it measured faster)
+// Per-unit compile choices (build.py UNIT_FLAGS; each measured per config):
+// MRP_LANES_PAIRS=1   the lanes-path sweeps two per loop trip (v0, v3)
+// MRP_VEL_PICK2=1     the block solver's case tests as two ballots of the compares (no bool in a VGPR)
+// MRP_VEL_VTCROSS=1   the tangent speed b2Dot(dv, (n.y, -n.x)) as dv.x*n.y - dv.y*n.x (pcross: a + (-b) is
+//                     a - b exactly), so the tangent is never materialised for it
+// MRP_VEL_BFREE=1     the block solver's four cases evaluated together and picked by per-lane selects
+//                     (no chain of case tests, no ballot -> branch); MRP_VEL_BFREE_LANES=1 restricts it to
+//                     the lanes path (3+ contacts)
+// MRP_FRESH_REGS=1    values k_step needs late in the step are made where they are used (v0, v3)
+// MRP_ONE_ROT=0       the position passes of a V == 0 unit (v0, Heavy-v0) keep the rotation memo instead
+//                     of the ONE_ROT form (World::ONE_ROT)
+// Diagnostic builds (never shipped): MRP_STAMPS (+ MRP_STAMPS_TOI) per-phase timing, MRP_PROGRESS
+// hang localisation.  The arms measured and dropped in rounds 3-5 are kept as patches under
+// profiles/ (r6_dropped_arms.patch), not in this header.
 #ifndef MRP_LANES_PAIRS
 #define MRP_LANES_PAIRS 0
 #endif
-// Velocity-update variants (round 5 A/B; each keeps every float operation and its order):
-// MRP_VEL_PICK2  the block solver's case tests as two ballots of the compares (no bool in a VGPR)
-// MRP_VEL_VTCROSS  the tangent speed b2Dot(dv, (n.y, -n.x)) as dv.x*n.y - dv.y*n.x (pcross: a + (-b) is
-//                a - b exactly), so the tangent is never materialised for it
-// MRP_VEL_EXPECT  case 1 of the block solver (both points active) laid out as the fall-through path
-// MRP_VEL_SPLIT  case 1 applies its impulse on a path of its own (no join with the rarer cases)
-// MRP_VEL_SPEC   case 1 applied speculatively, its test resolved afterwards (restore + cases 2-4 if not)
-// MRP_VEL_BFREE  the four cases evaluated together and picked by selects (no chain of case tests)
-#ifndef MRP_XW_LATE
-#define MRP_XW_LATE 0
-#endif
-#ifndef MRP_XW_LATE_POS
-#define MRP_XW_LATE_POS 0
-#endif
-#ifndef MRP_XW_PAIRS
-#define MRP_XW_PAIRS 0
+#ifndef MRP_ONE_ROT
+#define MRP_ONE_ROT 1
 #endif
 #ifndef MRP_VEL_PICK2
 #define MRP_VEL_PICK2 0
@@ -83,33 +67,14 @@ constexpr int NULLN = -1;
 #ifndef MRP_VEL_VTCROSS
 #define MRP_VEL_VTCROSS 0
 #endif
-#ifndef MRP_VEL_EXPECT
-#define MRP_VEL_EXPECT 0
-#endif
-#ifndef MRP_VEL_SPLIT
-#define MRP_VEL_SPLIT 0
-#endif
-#ifndef MRP_VEL_SPEC
-#define MRP_VEL_SPEC 0
-#endif
 #ifndef MRP_VEL_BFREE
 #define MRP_VEL_BFREE 0
 #endif
 #ifndef MRP_VEL_BFREE_LANES
 #define MRP_VEL_BFREE_LANES 0
 #endif
-// MRP_FRESH_REGS=1: values k_step needs late in the step (the state store's per-thread offsets, the
-// TOI phase's zeroes) are made where they are used, so they are not live across the step (v0 spilled
-// them to scratch: 8 of its 14 VGPR spills)
 #ifndef MRP_FRESH_REGS
 #define MRP_FRESH_REGS 0
-#endif
-#if MRP_VEL_EXPECT
-#define MRP_UNLIKELY(c) __builtin_expect(!!(c), 0)
-#define MRP_LIKELY(c) __builtin_expect(!!(c), 1)
-#else
-#define MRP_UNLIKELY(c) (c)
-#define MRP_LIKELY(c) (c)
 #endif
 #if MRP_VEL_VTCROSS
 #define MRP_VT(dv, n, t) pcross(dv, n)
@@ -118,16 +83,6 @@ constexpr int NULLN = -1;
 #else
 #define MRP_VT(dv, n, t) pdot(dv, t)
 #define MRP_PT(l, n, t) (pbc(l) * (t))
-#endif
-#ifdef MRP_XW_INLINE
-#define MRP_XW_FN __device__ __forceinline__
-#else
-#define MRP_XW_FN __device__ __attribute__((noinline))
-#endif
-#ifdef MRP_SOLVE_NOINLINE_MAIN
-#define MRP_MAIN_FN __device__ __attribute__((noinline))
-#else
-#define MRP_MAIN_FN __device__ __forceinline__
 #endif
 
 // v_writelane_b32 (clang exposes no builtin for it; the LLVM intrinsic is bound by name, so the
@@ -143,13 +98,16 @@ static __device__ unsigned long long g_stamps[16];     // per-phase sums over la
 static __device__ unsigned long long g_pmax[16];       // per-phase max over lane-steps
 static __device__ unsigned long long g_stepmax[256];   // per step (stepCounter mod 256): slowest lane's total
 static __device__ unsigned long long g_rt[2];          // sums of lane totals: s_memtime ticks, s_memrealtime ticks
-constexpr int MRP_TRACE_W = 32;   // include/mrp.h MRP_TRACE_WORDS (static_assert in mrp_lane.h)
+constexpr int MRP_TRACE_W = 40;   // include/mrp.h MRP_TRACE_WORDS (static_assert in mrp_lane.h)
 static __device__ uint32_t g_trace[16384][MRP_TRACE_W];   // last step per lane: phases 0-10, total, nc, toi, pos, vel-units,
                                                        // velocity / position / island-set-up cycles, largest island,
                                                        // 20/21 TOI split (candidate scan + b2TimeOfImpact, events),
                                                        // 22/23 collide split (narrow phase, serial commit), 24-26 load
                                                        // sub-phases (state, tables, barrier), 27 step index mod 256,
-                                                       // 28/29 s_memrealtime at entry / end, 30/31 HW_ID / XCC_ID
+                                                       // 28/29 s_memrealtime at entry / end, 30/31 HW_ID / XCC_ID,
+                                                       // 32 island building (DFS), 33 island write-back and
+                                                       // integration (island_mid / island_post), 34 fixture
+                                                       // synchronisation after the solve, 35 the TOI scan alone
 #define MRP_NOW() __builtin_amdgcn_s_memtime()
 #define MRP_SUB(k, t0) do { if (tid == 0) sh.trace[k] += (uint32_t)(__builtin_amdgcn_s_memtime() - (t0)); } while (0)
 #define MRP_TRACE(k, v) do { if (tid == 0) sh.trace[k] += (v); } while (0)
@@ -314,8 +272,6 @@ template <int ENV> struct Shared {
     LS S;
     LdsTables<ENV> lt;
     IslT<NBODY, C> isl;
-    int stack[NBODY];
-    int isl_go;
     int hw_io;   // LaneState::cHW as k_step loaded it (its store writes slots < max(hw_io, cHW) back)
     float salpha0[4];
     // collide: contact list snapshot (the per-contact manifolds live in the phase union below)
@@ -351,6 +307,7 @@ template <int ENV> struct Shared {
         } col;
         uint8_t pover[LS::TN * (LS::TN - 1) / 2];
         struct { SweepV tsA[C], tsB[C]; TOIOut tout[C]; } toi;
+        struct { float lx[D::NF], ly[D::NF], hx[D::NF], hy[D::NF], dx[D::NF], dy[D::NF]; } fsync;   // solve_coop's end
     } u;
     // env I/O
     float obs[D::OBS];
@@ -360,7 +317,7 @@ template <int ENV> struct Shared {
     double draws[D::NDRAW];
     unsigned long long stamp_t, stamp_t0, stamp_rt0;
 #ifdef MRP_STAMPS
-    uint32_t trace[32];
+    uint32_t trace[MRP_TRACE_W];
 #endif
 };
 
@@ -559,6 +516,10 @@ template <int ENV> struct World {
     }
     __device__ __forceinline__ void move_proxy(int id, float lx, float ly, float hx, float hy, V2 disp) {
         if (S.tlx[id] <= lx && S.tly[id] <= ly && hx <= S.thx[id] && hy <= S.thy[id]) return;   // Contains
+        move_proxy_out(id, lx, ly, hx, hy, disp);
+    }
+    // b2DynamicTree::MoveProxy past its Contains test: reinsert the leaf with its new fat AABB
+    __device__ __forceinline__ void move_proxy_out(int id, float lx, float ly, float hx, float hy, V2 disp) {
         t_remove(id);
         float blx = lx - AABB_EXT, bly = ly - AABB_EXT, bhx = hx + AABB_EXT, bhy = hy + AABB_EXT;
         V2 d = vmul(AABB_MUL, disp);
@@ -574,6 +535,48 @@ template <int ENV> struct World {
         if (d1x > 0.0f || d1y > 0.0f) return false;
         if (d2x > 0.0f || d2y > 0.0f) return false;
         return true;
+    }
+    // b2Body::SynchronizeFixtures of every body flagged in `bflag` (b2World::Solve's end), on the whole
+    // wave: lane f takes fixture f's swept AABB (its body's transform at the sweep start and now, the
+    // float operations of sync_fixtures) and b2DynamicTree::MoveProxy's Contains test; a leaf's fat AABB
+    // changes only in its own MoveProxy, so the test does not depend on the moves before it.  Thread 0
+    // then reinserts the leaves that left their fat AABBs, in the reference's order (bodies from the
+    // last created, fixtures newest first), which is the order the tree's shape depends on.
+    __device__ __forceinline__ void sync_fixtures_coop(uint32_t bflag) {
+        static_assert(NF <= 64, "one lane per fixture");
+        const unsigned long long tf = MRP_NOW();
+        const int f = tid < NF ? tid : 0;
+        const int b = L.fix_body[f];
+        const bool act = tid < NF && b < ND && ((bflag >> b) & 1u);
+        bool out = false;
+        if (act) {
+            Xf x1; x1.q = rot(S.a0[b]);
+            x1.p = vsub(v2(S.c0x[b], S.c0y[b]), mul_rv(x1.q, lc(b)));
+            const Xf x2 = xf(b);
+            float l1x, l1y, h1x, h1y, l2x, l2y, h2x, h2y;
+            poly_aabb(L.shape[f], x1, l1x, l1y, h1x, h1y);
+            poly_aabb(L.shape[f], x2, l2x, l2y, h2x, h2y);
+            const V2 disp = vsub(x2.p, x1.p);
+            const float lx = fmin_(l1x, l2x), ly = fmin_(l1y, l2y), hx = fmax_(h1x, h2x), hy = fmax_(h1y, h2y);
+            const int id = S.proxy[f];
+            out = !(S.tlx[id] <= lx && S.tly[id] <= ly && hx <= S.thx[id] && hy <= S.thy[id]);   // not Contains
+            sh.u.fsync.lx[f] = lx; sh.u.fsync.ly[f] = ly; sh.u.fsync.hx[f] = hx; sh.u.fsync.hy[f] = hy;
+            sh.u.fsync.dx[f] = disp.x; sh.u.fsync.dy[f] = disp.y;
+        }
+        const uint64_t moves = __builtin_amdgcn_ballot_w64(out);
+        __syncthreads();
+        if (tid == 0 && moves != 0ull) {
+            for (int bb = ND - 1; bb >= 0; --bb) {
+                if (!(bflag & (1u << bb))) continue;
+                for (int k = L.body_nfix[bb] - 1; k >= 0; --k) {
+                    const int ff = L.body_fix0[bb] + k;
+                    if ((moves >> ff) & 1ull)
+                        move_proxy_out(S.proxy[ff], sh.u.fsync.lx[ff], sh.u.fsync.ly[ff], sh.u.fsync.hx[ff], sh.u.fsync.hy[ff],
+                                       v2(sh.u.fsync.dx[ff], sh.u.fsync.dy[ff]));
+                }
+            }
+        }
+        MRP_SUB(34, tf);
     }
     // b2Body::SynchronizeFixtures for a dynamic body, fixtures in fixture-list order (newest first)
     __device__ __forceinline__ void sync_fixtures(int b) {
@@ -846,7 +849,7 @@ template <int ENV> struct World {
         const int n = sh.ccount;
         // up to 32 contacts: a group of G = 8, 4 or 2 lanes per contact shares its SAT edge scans
         // (collide_polygons with G > 1); more: one lane per contact
-        const int G = MRP_COLLIDE_GROUPS ? (n <= 8 ? 8 : (n <= 16 ? 4 : (n <= 32 ? 2 : 1))) : 1;
+        const int G = n <= 8 ? 8 : (n <= 16 ? 4 : (n <= 32 ? 2 : 1));
         if (G > 1) {
             const int g = tid / G, sub = tid & (G - 1);
             if (g < n) {
@@ -898,9 +901,6 @@ template <int ENV> struct World {
 
     // wave issue priority (s_setprio takes an immediate); `level` must be wave-uniform
     __device__ __forceinline__ static void set_prio(int level) {
-#ifdef MRP_NO_PRIO   // experiment switch: every wave at the default priority
-        return;
-#endif
         level = __builtin_amdgcn_readfirstlane(level);
         if (level >= 3) __builtin_amdgcn_s_setprio(3);
         else if (level == 2) __builtin_amdgcn_s_setprio(2);
@@ -1191,18 +1191,16 @@ template <int ENV> struct World {
     // whenever k and iters have the same parity.  The state is compared at the k with
     // iters - k = 0 mod 4 against a snapshot taken two sweeps earlier (every fourth sweep rather
     // than every second: the comparison is off the sweeps' dependency chain but not free).
-#ifndef MRP_SCHED_WIDE_AGENTS
-#define MRP_SCHED_WIDE_AGENTS 5   // Heavy-v0 (5 agents): +5.9 % in the driver window (profiles/r3g_ab_envs_1_2_5.txt)
-#endif
-    // envs whose islands reach 5-8 contacts (several blocks, or 5 agents) get scheduled sweeps for those too
-    static constexpr bool SCHED_WIDE = NB > 1 || NA >= MRP_SCHED_WIDE_AGENTS;
+    // envs whose islands reach 5-8 contacts (several blocks, or 5 agents: Heavy-v0 +5.9 % in the driver
+    // window, profiles/r3g_ab_envs_1_2_5.txt) get scheduled sweeps for those too
+    static constexpr bool SCHED_WIDE = NB > 1 || NA >= 5;
     // islands of NC = 3 or 4 contacts (the slowest lanes' islands): the contacts' bodies and point
     // counts are read out of their lanes once, before the sweeps, into scalar registers, and the
     // contact loop is unrolled, so a contact update issues no readlane for its schedule and the body
     // readlanes take a lane select written long before (no wait states); same operations and order as
     // the generic loop below
     template <int NC>
-    MRP_LANES_FN int lanes_sweeps(Isl& is, VC* vcs, int iters, bool early_exit, int stop = 1 << 30, bool* exited = nullptr) {
+    MRP_LANES_FN int lanes_sweeps(Isl& is, VC* vcs, int iters, bool early_exit) {
         const int me = tid < NC ? tid : 0;
         CC my = load_cc(vcs[me]);
         const int cia = vcs[me].iaI, cib = vcs[me].ibI;
@@ -1231,9 +1229,7 @@ template <int ENV> struct World {
         P2 sni = my.ni, sti = my.ti;
         float sbx = bvx, sby = bvy, sbw = bw;
         bool have = ((iters - sweeps) & 3) == 2;   // the start is a snapshot point
-        const int last = stop < iters ? stop : iters;
-        bool ex = false;
-        while (sweeps < last) {
+        while (sweeps < iters) {
             sweep();
             if (STEP == 2) sweep();
             sweeps += STEP;
@@ -1243,7 +1239,7 @@ template <int ENV> struct World {
                                    (__float_as_uint(my.ti.x) ^ __float_as_uint(sti.x)) | (__float_as_uint(my.ti.y) ^ __float_as_uint(sti.y)) |
                                    (__float_as_uint(bvx) ^ __float_as_uint(sbx)) | (__float_as_uint(bvy) ^ __float_as_uint(sby)) |
                                    (__float_as_uint(bw) ^ __float_as_uint(sbw));
-                if (__builtin_amdgcn_ballot_w64(d != 0u) == 0) { ex = true; break; }
+                if (__builtin_amdgcn_ballot_w64(d != 0u) == 0) break;
             }
             if (early_exit && (left & m) == 2) {
                 sni = my.ni; sti = my.ti; sbx = bvx; sby = bvy; sbw = bw;
@@ -1252,34 +1248,13 @@ template <int ENV> struct World {
         }
         if (tid < is.nb) { is.vvx[tid] = bvx; is.vvy[tid] = bvy; is.vw[tid] = bw; }
         if (tid < NC) store_cc(vcs[tid], my);
-        if (exited) *exited = ex || sweeps >= iters;
         return sweeps;
     }
-    template <int NC>
-    MRP_MAIN_FN int lanes_sweeps_main(Isl& is, VC* vcs, int iters, bool early_exit) {
-#if MRP_XW_LATE
-        // islands that have not repeated by sweep MRP_XW_LATE (the launches' slowest lanes: all 180
-        // sweeps) continue on the two-body register path when their shape has one; the others never
-        // pay its call (k_step's live registers saved around it), so short solves stay on the lanes path
-        if constexpr (XW_LATE_OK) {
-            const XwShape q = xw_shape(is, vcs);
-            if (xw_supported(q.key)) {
-                bool done = false;
-                const int k = lanes_sweeps<NC>(is, vcs, iters, early_exit, MRP_XW_LATE, &done);
-                if (done) return k;
-                return solver_velocity_xw_from(is, vcs, iters, early_exit, q, k);
-            }
-        }
-#endif
-        return lanes_sweeps<NC>(is, vcs, iters, early_exit);
-    }
-    // MAIN: the call of the main island solve (b2Island::Solve), not a TOI sub-step's
-    template <bool MAIN = false>
     __device__ __forceinline__ int solver_velocity_lanes(Isl& is, VC* vcs, int iters, bool early_exit = true) {
         {
             const int n = __builtin_amdgcn_readfirstlane(is.nc);
-            if (n == 3) return MAIN ? lanes_sweeps_main<3>(is, vcs, iters, early_exit) : lanes_sweeps<3>(is, vcs, iters, early_exit);
-            if (n == 4) return MAIN ? lanes_sweeps_main<4>(is, vcs, iters, early_exit) : lanes_sweeps<4>(is, vcs, iters, early_exit);
+            if (n == 3) return lanes_sweeps<3>(is, vcs, iters, early_exit);
+            if (n == 4) return lanes_sweeps<4>(is, vcs, iters, early_exit);
             if constexpr (SCHED_WIDE) {   // islands of 5-8 contacts (the 3-block config: +4 %)
                 if (n == 5) return lanes_sweeps<5>(is, vcs, iters, early_exit);
                 if (n == 6) return lanes_sweeps<6>(is, vcs, iters, early_exit);
@@ -1347,7 +1322,6 @@ template <int ENV> struct World {
     struct PickUni {
         static constexpr bool LANES = false;
         __device__ __forceinline__ bool operator()(bool c) const { return uni(c); }
-        __device__ __forceinline__ bool mask(uint64_t m) const { return m != 0ull; }   // m: a ballot
         __device__ __forceinline__ bool both(bool a, bool b) const {
 #if MRP_VEL_PICK2
             return (__builtin_amdgcn_ballot_w64(a) & __builtin_amdgcn_ballot_w64(b)) != 0ull;
@@ -1360,7 +1334,6 @@ template <int ENV> struct World {
         static constexpr bool LANES = true;
         int i;
         __device__ __forceinline__ bool operator()(bool c) const { return lane_bit(c, i); }
-        __device__ __forceinline__ bool mask(uint64_t m) const { return (m >> i) & 1ull; }
         __device__ __forceinline__ bool both(bool a, bool b) const {
 #if MRP_VEL_PICK2
             return ((__builtin_amdgcn_ballot_w64(a) & __builtin_amdgcn_ballot_w64(b)) >> i) & 1ull;
@@ -1489,10 +1462,7 @@ template <int ENV> struct World {
                 wB += iB * (pcrossp(c.rB0, P1) + pcrossp(c.rB1, P2v));
                 ni = xs;
             };
-#if MRP_VEL_BFREE
-            // MRP_VEL_BFREE_LANES: the selects on the lanes path only (3+ contacts); the register paths
-            // (one and two contacts, mostly case-1 updates) keep the case loop below
-            if constexpr (!MRP_VEL_BFREE_LANES || Pick::LANES) {
+            if constexpr (MRP_VEL_BFREE && (!MRP_VEL_BFREE_LANES || Pick::LANES)) {
                 // All four cases evaluated at once and the first that holds picked by selects, in Box2D's
                 // order (both points active; point 1 only; point 2 only; none), so no case test waits on
                 // the one before it.  The launches' slowest lanes mostly run the later cases (v0: 72 %
@@ -1504,7 +1474,6 @@ template <int ENV> struct World {
                 P2 xs;
                 xs.x = c1 ? x.x : (c2 ? x2 : 0.0f);
                 xs.y = c1 ? x.y : (c2 ? 0.0f : (c3 ? x3 : 0.0f));
-#if MRP_VEL_BFREE >= 2
                 // whether any case holds picked per lane as well: the impulse is applied unconditionally and
                 // each output selected between the applied and the incoming value (the same bits either
                 // way), so no ballot -> scalar -> branch sits on the chain.  Every lane decides from its
@@ -1518,17 +1487,9 @@ template <int ENV> struct World {
                 vB.x = any ? vB.x : vB0.x; vB.y = any ? vB.y : vB0.y; wB = any ? wB : wB0;
                 ni.x = any ? ni.x : ni0.x; ni.y = any ? ni.y : ni0.y;
                 (void)pick;
-#else
-                // some case holds (else Box2D gives up and leaves the contact unchanged): one ballot per compare
-                const uint64_t ok = (__builtin_amdgcn_ballot_w64(x.x >= 0.0f) & __builtin_amdgcn_ballot_w64(x.y >= 0.0f)) |
-                                    (__builtin_amdgcn_ballot_w64(x2 >= 0.0f) & __builtin_amdgcn_ballot_w64(v2 >= 0.0f)) |
-                                    (__builtin_amdgcn_ballot_w64(x3 >= 0.0f) & __builtin_amdgcn_ballot_w64(v3 >= 0.0f)) |
-                                    (__builtin_amdgcn_ballot_w64(b.x >= 0.0f) & __builtin_amdgcn_ballot_w64(b.y >= 0.0f));
-                if (pick.mask(ok)) apply(xs);
-#endif
             } else {
                 bool ok = true;
-                if (MRP_UNLIKELY(!pick.both(x.x >= 0.0f, x.y >= 0.0f))) {
+                if (!pick.both(x.x >= 0.0f, x.y >= 0.0f)) {
                     x.x = -c.nmass0 * b.x; x.y = 0.0f;
                     vn2 = c.k01.y * x.x + b.y;
                     if (!pick.both(x.x >= 0.0f, vn2 >= 0.0f)) {
@@ -1542,59 +1503,7 @@ template <int ENV> struct World {
                 }
                 if (ok) apply(x);
             }
-#elif MRP_VEL_SPEC
-            // case 1 (both points active) applied speculatively, its test resolved after the
-            // application: the branch leaves the dependency chain.  When case 1 does not hold, the
-            // velocities and impulses are restored and cases 2-4 run as the reference orders them
-            // (same operations on the same inputs, so the same bits).
-            const P2 vA0 = vA, vB0 = vB;
-            const float wA0 = wA, wB0 = wB;
-            const bool c1 = pick.both(x.x >= 0.0f, x.y >= 0.0f);
-            apply(x);
-            asm volatile("" :: "v"(vA), "v"(vB), "v"(wA), "v"(wB), "v"(ni));   // computed before the test: no sinking
-            if (MRP_UNLIKELY(!c1)) {
-                vA = vA0; vB = vB0; wA = wA0; wB = wB0; ni = a;
-                vel_block_rare(c, pick, b, vn1, vn2, apply);
-            }
-#elif MRP_VEL_SPLIT
-            // case 1 (both points active) is the straight path; the other cases branch off it and
-            // carry their own copy of the impulse application, so the common path has no join
-            if (MRP_LIKELY(pick.both(x.x >= 0.0f, x.y >= 0.0f))) {
-                apply(x);
-            } else {
-                vel_block_rare(c, pick, b, vn1, vn2, apply);
-            }
-#else
-            bool ok = true;
-            if (MRP_UNLIKELY(!pick.both(x.x >= 0.0f, x.y >= 0.0f))) {
-                x.x = -c.nmass0 * b.x; x.y = 0.0f;
-                vn2 = c.k01.y * x.x + b.y;
-                if (!pick.both(x.x >= 0.0f, vn2 >= 0.0f)) {
-                    x.x = 0.0f; x.y = -c.nmass1 * b.y;
-                    vn1 = c.k01.y * x.y + b.x;
-                    if (!pick.both(x.y >= 0.0f, vn1 >= 0.0f)) {
-                        x.x = 0.0f; x.y = 0.0f;
-                        ok = pick.both(b.x >= 0.0f, b.y >= 0.0f);
-                    }
-                }
-            }
-            if (ok) apply(x);
-#endif
         }
-    }
-    // cases 2-4 of the block solver (b2ContactSolver::SolveVelocityConstraints), each with its own
-    // application of the impulse (MRP_VEL_SPLIT)
-    template <class Pick, class Apply>
-    __device__ __forceinline__ static void vel_block_rare(const CC& c, Pick pick, const P2 b, float vn1, float vn2, Apply apply) {
-        P2 x;
-        x.x = -c.nmass0 * b.x; x.y = 0.0f;
-        vn2 = c.k01.y * x.x + b.y;
-        if (pick.both(x.x >= 0.0f, vn2 >= 0.0f)) { apply(x); return; }
-        x.x = 0.0f; x.y = -c.nmass1 * b.y;
-        vn1 = c.k01.y * x.y + b.x;
-        if (pick.both(x.y >= 0.0f, vn1 >= 0.0f)) { apply(x); return; }
-        x.x = 0.0f; x.y = 0.0f;
-        if (pick.both(b.x >= 0.0f, b.y >= 0.0f)) apply(x);
     }
     // the register-resident form: identical lanes, every lane keeps the result
     template <int PC>
@@ -1640,34 +1549,27 @@ template <int ENV> struct World {
     };
     // The early-exit schedule: after sweep k (left = iters - k) the state is compared with the
     // snapshot taken two sweeps earlier when left = 0 mod M, and a snapshot is taken when
-    // left = 2 mod M, with M = 4 for the first MRP_EXIT_DENSE sweeps and M = MRP_EXIT_SPARSE after
+    // left = 2 mod M, with M = 4 for the first EXIT_DENSE sweeps and M = EXIT_SPARSE after
     // (both powers of two, so a compare point of either phase has its snapshot exactly two sweeps
     // before it: left + 2 = 2 mod 4 and mod M).  Any such schedule exits exactly (the state then
     // has period 1 or 2 and iters - k is even); most islands that repeat do so within a few
     // sweeps, and the islands that never repeat (the launch's slowest lanes) pay the snapshot and
     // compare once per M sweeps instead of once per 4.
-#ifndef MRP_EXIT_DENSE
-#define MRP_EXIT_DENSE 32
-#endif
-#ifndef MRP_EXIT_SPARSE
-#define MRP_EXIT_SPARSE 16
-#endif
-    static_assert(MRP_EXIT_SPARSE >= 4 && (MRP_EXIT_SPARSE & (MRP_EXIT_SPARSE - 1)) == 0, "a power of two >= 4");
-    __device__ __forceinline__ static int exit_mask(int done) { return done > MRP_EXIT_DENSE ? MRP_EXIT_SPARSE - 1 : 3; }
+    static constexpr int EXIT_DENSE = 32, EXIT_SPARSE = 16;   // profiles/r4_ab_sparse_exit.txt
+    static_assert(EXIT_SPARSE >= 4 && (EXIT_SPARSE & (EXIT_SPARSE - 1)) == 0, "a power of two >= 4");
+    __device__ __forceinline__ static int exit_mask(int done) { return done > EXIT_DENSE ? EXIT_SPARSE - 1 : 3; }
     __device__ __forceinline__ static bool snap_initial(int iters) { return (iters & 3) == 2; }   // sweep 0 is a snapshot point
     // The sweep loop of the register paths: `sweep()` runs one Gauss-Seidel sweep, `state(v)` names
     // the NS values of the sweep state.  Every compare point has iters - k even, so the sweeps run in
     // pairs and the loop carries no per-sweep parity test or exit bookkeeping (an odd count runs its
     // first sweep alone); returns the sweeps run.
-    // `start` > 0: continuing after `start` sweeps of another path whose last compare point was sweep
-    // `start` (MRP_XW_LATE; even, as every compare point is): no snapshot is held yet
     template <int NS, class Sweep, class State>
-    __device__ __forceinline__ static int sweep_pairs(int iters, bool early_exit, Sweep sweep, State state, int start = 0) {
-        int it = start;
-        if ((iters - start) & 1) { sweep(); it += 1; }
+    __device__ __forceinline__ static int sweep_pairs(int iters, bool early_exit, Sweep sweep, State state) {
+        int it = 0;
+        if (iters & 1) { sweep(); it += 1; }
         float cur[NS];
         state(cur);
-        Snap<NS> snap(cur, start == 0 && ((iters - it) & 3) == 2);
+        Snap<NS> snap(cur, ((iters - it) & 3) == 2);
         while (it < iters) {
             sweep();
             sweep();
@@ -1766,155 +1668,6 @@ template <int ENV> struct World {
                        : solver_velocity_two_p<1, 1>(is, vcs, iters, early_exit);
     }
 
-    // ---------------------------------------------------------------- two-body register paths, 3-4 contacts
-    // The slowest v0 lanes solve islands of 3 or 4 contacts on at most two moving bodies: X, the block,
-    // is A of every contact, against an agent Y (both boxes of the T touch it) and one or two walls
-    // (round 4 capture of the launches' slowest lane-steps, profiles/r4_issue_roofline.json).  On such a
-    // shape every contact is (X, Y) or (X, W) with W static, and MASK (bit i: contact i is (X, W)) is a
-    // template parameter, so every body access is a register and no velocity goes through readlane /
-    // writelane (the lanes path pays 12 readlanes, 6 writelanes and their wait states per update).
-    // A static body's velocity is +0 before and after each update (invMass = invI = 0, so v - 0 * P = +0
-    // and w - 0 * x = +0 for a finite impulse; a non-finite one marks the lane non-finite), so W is a
-    // zero per update and is not written back; X and Y take their inverse masses from the contacts
-    // (the same bits the solver copied into every contact of the body).  Point counts stay runtime
-    // (one wave-uniform branch per update).  Same float operations in the same order as
-    // solver_velocity, same exact early exit as the other register paths.
-#ifdef MRP_XW_PATHS
-    static constexpr bool XW_PATHS = ENV == 0;
-#else
-    // measured (round 4, profiles/r4_ab_xw.txt): +0.5 % in the driver window, -4 % at steps 21-220 and
-    // -6 % over a whole episode (the call and its register saves per island solve); off by default
-    static constexpr bool XW_PATHS = false;
-#endif
-    // MRP_XW_LATE=N (sweeps) / MRP_XW_LATE_POS=N (passes): the main island solve's 3-4 contact islands
-    // of a two-body shape run the lanes path for N sweeps (passes) and, when they have not exited by then,
-    // the two-body register path for the rest (the call is paid only by the long solves)
-    static constexpr bool XW_LATE_OK = ENV == 0 && (MRP_XW_LATE > 0 || MRP_XW_LATE_POS > 0);
-    __device__ __forceinline__ static void xw_update(CC& c, bool wall, bool two, const P2 mX, const float iX, const P2 mY,
-                                                     const float iY, P2& vX, float& wX, P2& vY, float& wY) {
-        asm volatile("" : "+v"(c.normal));   // as cc_update: the tangent formed inside the packed instructions
-        P2 ni, ti;
-        PickUni pick;
-        if (wall) {
-            P2 vW = p2(0.0f, 0.0f);
-            float wW = 0.0f;
-            if (two) vel_update_m<2>(c, mX, iX, pbc(0.0f), 0.0f, pick, ni, ti, vX, wX, vW, wW);
-            else vel_update_m<1>(c, mX, iX, pbc(0.0f), 0.0f, pick, ni, ti, vX, wX, vW, wW);
-        } else {
-            if (two) vel_update_m<2>(c, mX, iX, mY, iY, pick, ni, ti, vX, wX, vY, wY);
-            else vel_update_m<1>(c, mX, iX, mY, iY, pick, ni, ti, vX, wX, vY, wY);
-        }
-        c.ni = ni; c.ti = ti;
-    }
-    template <int MASK, int NC> static constexpr int xw_first_y() {
-        for (int i = 0; i < NC; ++i)
-            if (!((MASK >> i) & 1)) return i;
-        return -1;
-    }
-    template <int NC, int MASK>
-    MRP_XW_FN int sweep_xw(Isl& is, VC* vcs, int iters, bool early_exit, int x, int y, int pcm, int start = 0) {
-        constexpr int FY = xw_first_y<MASK, NC>();
-        constexpr int NS = 6 + 4 * NC;
-        CC c[NC];
-#pragma unroll
-        for (int i = 0; i < NC; ++i) c[i] = load_cc(vcs[i]);
-        const P2 mX = c[0].mA;
-        const float iX = c[0].iA;
-        const P2 mY = FY >= 0 ? c[FY >= 0 ? FY : 0].mB : pbc(0.0f);
-        const float iY = FY >= 0 ? c[FY >= 0 ? FY : 0].iB : 0.0f;
-        P2 vX = p2(is.vvx[x], is.vvy[x]), vY = p2(0.0f, 0.0f);
-        float wX = is.vw[x], wY = 0.0f;
-        if (FY >= 0) { vY = p2(is.vvx[y], is.vvy[y]); wY = is.vw[y]; }
-        auto state = [&](float (&v)[NS]) {
-            v[0] = vX.x; v[1] = vX.y; v[2] = wX; v[3] = vY.x; v[4] = vY.y; v[5] = wY;
-#pragma unroll
-            for (int i = 0; i < NC; ++i) { v[6 + 4 * i] = c[i].ni.x; v[7 + 4 * i] = c[i].ni.y; v[8 + 4 * i] = c[i].ti.x; v[9 + 4 * i] = c[i].ti.y; }
-        };
-#if MRP_XW_PAIRS
-        // two sweeps per loop trip, the exit bookkeeping once per pair (as the one- and two-contact
-        // register paths: sweep_pairs)
-        const int sweeps = sweep_pairs<NS>(iters, early_exit, [&] {
-#pragma unroll
-            for (int i = 0; i < NC; ++i) xw_update(c[i], (MASK >> i) & 1, (pcm >> i) & 1, mX, iX, mY, iY, vX, wX, vY, wY);
-        }, state, start);
-#else
-        float init[NS];
-        state(init);
-        // start > 0: continuing the lanes path's sweeps (MRP_XW_LATE); its last compare point was
-        // sweep `start`, so no snapshot is held and the schedule resumes at the next snapshot point
-        Snap<NS> snap(init, start == 0 ? snap_initial(iters) : false);
-        int sweeps = start;
-        for (int it = start; it < iters; ++it) {
-            ++sweeps;
-#pragma unroll
-            for (int i = 0; i < NC; ++i) xw_update(c[i], (MASK >> i) & 1, (pcm >> i) & 1, mX, iX, mY, iY, vX, wX, vY, wY);
-            if (early_exit && ((iters - it - 1) & 1) == 0) {
-                float cur[NS];
-                state(cur);
-                if (snap.step(it, iters, cur)) break;
-            }
-        }
-#endif
-        if (tid == 0) {
-            is.vvx[x] = vX.x; is.vvy[x] = vX.y; is.vw[x] = wX;
-            if (FY >= 0) { is.vvx[y] = vY.x; is.vvy[y] = vY.y; is.vw[y] = wY; }
-#pragma unroll
-            for (int i = 0; i < NC; ++i) store_cc(vcs[i], c[i]);
-        }
-        return sweeps;
-    }
-    // the island's shape for the two-body paths: (NC, MASK) packed as NC * 16 + MASK with X and Y and
-    // the point-count mask, or -1 when a contact is not (X, Y) / (X, static) or NC is not 3 or 4
-    struct XwShape { int key, x, y, pcm; };
-    __device__ __forceinline__ XwShape xw_shape(const Isl& is, const VC* vcs) const {
-        XwShape r{-1, 0, -1, 0};
-        const int nc = __builtin_amdgcn_readfirstlane(is.nc);
-        if (nc != 3 && nc != 4) return r;
-        const int x = __builtin_amdgcn_readfirstlane(vcs[0].iaI);
-        if (!is_dyn(is.bodies[x])) return r;
-        int y = -1, mask = 0, pcm = 0;
-        for (int i = 0; i < nc; ++i) {
-            const int a = __builtin_amdgcn_readfirstlane(vcs[i].iaI), b = __builtin_amdgcn_readfirstlane(vcs[i].ibI);
-            if (a != x) return r;
-            if (is_dyn(__builtin_amdgcn_readfirstlane(is.bodies[b]))) {
-                if (y >= 0 && b != y) return r;
-                y = b;
-            } else {
-                mask |= 1 << i;
-            }
-            if (__builtin_amdgcn_readfirstlane(vcs[i].pointCount) == 2) pcm |= 1 << i;
-        }
-        r.key = nc * 16 + mask; r.x = x; r.y = y; r.pcm = pcm;
-        return r;
-    }
-    // the shapes instantiated (the v0 driver window's 3-4 contact islands, by velocity updates: (3, 4)
-    // 24 %, (3, 7) 14 %, (4, 15) 13 %, (3, 6) 9 %, (4, 12) 8 %; oracle b2o_topo_diag, round 4)
-    __device__ __forceinline__ static bool xw_supported(int key) {
-        return key == 3 * 16 + 4 || key == 3 * 16 + 6 || key == 3 * 16 + 7 || key == 4 * 16 + 12 || key == 4 * 16 + 15;
-    }
-    // the same shapes, continuing after `start` sweeps of the lanes path (MRP_XW_LATE)
-    __device__ __forceinline__ int solver_velocity_xw_from(Isl& is, VC* vcs, int iters, bool early_exit, const XwShape q, int start) {
-        switch (q.key) {
-            case 3 * 16 + 4: return sweep_xw<3, 4>(is, vcs, iters, early_exit, q.x, q.y, q.pcm, start);
-            case 3 * 16 + 6: return sweep_xw<3, 6>(is, vcs, iters, early_exit, q.x, q.y, q.pcm, start);
-            case 3 * 16 + 7: return sweep_xw<3, 7>(is, vcs, iters, early_exit, q.x, q.y, q.pcm, start);
-            case 4 * 16 + 12: return sweep_xw<4, 12>(is, vcs, iters, early_exit, q.x, q.y, q.pcm, start);
-            default: return sweep_xw<4, 15>(is, vcs, iters, early_exit, q.x, q.y, q.pcm, start);
-        }
-    }
-    __device__ __forceinline__ int solver_velocity_xw(Isl& is, VC* vcs, int iters, bool early_exit = true) {
-        if constexpr (!XW_PATHS) return -1;
-        const XwShape q = xw_shape(is, vcs);
-        switch (q.key) {
-            case 3 * 16 + 4: return sweep_xw<3, 4>(is, vcs, iters, early_exit, q.x, q.y, q.pcm);
-            case 3 * 16 + 6: return sweep_xw<3, 6>(is, vcs, iters, early_exit, q.x, q.y, q.pcm);
-            case 3 * 16 + 7: return sweep_xw<3, 7>(is, vcs, iters, early_exit, q.x, q.y, q.pcm);
-            case 4 * 16 + 12: return sweep_xw<4, 12>(is, vcs, iters, early_exit, q.x, q.y, q.pcm);
-            case 4 * 16 + 15: return sweep_xw<4, 15>(is, vcs, iters, early_exit, q.x, q.y, q.pcm);
-            default: return -1;
-        }
-    }
-
     // ---------------------------------------------------------------- lane-distributed position iterations
     // b2ContactSolver::SolvePositionConstraints (toi = false) or SolveTOIPositionConstraints
     // (toi = true), repeated until the reference's exit test passes or `iters` passes have run,
@@ -1989,21 +1742,18 @@ template <int ENV> struct World {
     }
     // b2ContactSolver::SolvePositionConstraints (SolveTOIPositionConstraints) for one contact, with
     // the float operations and order of solver_position (each packed half is the scalar
-    // expression).  `getA` / `getB` give the rotation of an angle, called A then B per point as
-    // the reference sets xfA.q then xfB.q; `onSep(sep)` sees each point's separation.
-    template <class GetA, class GetB, class OnSep>
-    __device__ __forceinline__ static void pos_update(const PCC& c, int pcount, int type, float baum, GetA getA, GetB getB,
+    // expression).  `rots(aA, aB, qA, qB)` gives the bodies' rotations, b2Rot::Set of their angles
+    // (A then B per point, as the reference sets xfA.q then xfB.q); `onSep(sep)` sees each point's
+    // separation.
+    template <class Rots, class OnSep>
+    __device__ __forceinline__ static void pos_update(const PCC& c, int pcount, int type, float baum, Rots&& rots,
                                                       OnSep onSep, P2& cA, float& aA, P2& cB, float& aB) {
-        pos_update_m(c, c.mA, c.iA, c.mB, c.iB, pcount, type, baum, getA, getB, onSep, cA, aA, cB, aB);
-    }
-    // the same with the bodies' inverse masses / inertias passed in (see vel_update_m)
-    template <class GetA, class GetB, class OnSep>
-    __device__ __forceinline__ static void pos_update_m(const PCC& c, const P2 mA, const float iA, const P2 mB, const float iB,
-                                                        int pcount, int type, float baum, GetA getA, GetB getB,
-                                                        OnSep onSep, P2& cA, float& aA, P2& cB, float& aB) {
+        const P2 mA = c.mA, mB = c.mB;
+        const float iA = c.iA, iB = c.iB;
         for (int j = 0; j < 2; ++j) {
             if (j == pcount) break;
-            const P2 qA = getA(aA), qB = getB(aB);
+            P2 qA, qB;
+            rots(aA, aB, qA, qB);
             const P2 pA = cA - prot(qA, c.lcA), pB = cB - prot(qB, c.lcB);
             const P2 lp = j == 0 ? c.q0 : c.q1;
             P2 normal, point; float sep;
@@ -2034,12 +1784,37 @@ template <int ENV> struct World {
             aB += iB * pcross(rB, Pv);
         }
     }
-    // the register-resident form: identical lanes, one wave-uniform memo
+    // Rotations of a contact with at most one rotating body (invI != 0 after the TOI masking) in an
+    // island whose other bodies' angles are +0 (ONE_ROT islands: every island of v0 / Heavy-v0, whose
+    // agents have density 0, hence invI = 0, and spawn at angle 0, beside static walls).  A fixed
+    // body's angle stays +0 through the passes (a - 0 * x = +0 and a + 0 * x = +0 for every finite x;
+    // an infinite or NaN x makes it NaN), so its rotation is b2Rot::Set(+0) = {+0, 1} with no lookup.
+    // The rotating body's b2Rot::Set is evaluated at every point, straight-line: rot_fast is glibc's
+    // fast-reduction path, which rot() takes for |angle| < 120 rad.  `mx` keeps the largest |angle|
+    // bit pattern evaluated; the caller redoes any pass that met an angle of 120 rad or more, a NaN,
+    // or a fixed angle that went NaN, with b2Rot::Set of both angles through rot() (glibc's every
+    // branch), so every pass has the bits of the reference's (position-pass measurements:
+    // profiles/r6_posbench*.txt).  The other envs' islands (rotating agents) keep the rotation memo.
+    static constexpr bool ONE_ROT = MRP_ONE_ROT && D::V == 0;
+    static constexpr uint32_t ROT_FAST_END = 0x42f00000u;   // |angle| bits of 120.0f (rot(): abstop12 < that of 120)
+    __device__ __forceinline__ static void one_rot(bool rA, bool rB, float r, P2& qA, P2& qB, uint32_t& mx) {
+        const uint32_t m = __float_as_uint(r) & 0x7fffffffu;
+        mx = m > mx ? m : mx;
+        const Rot q = rot_fast(r);
+        const P2 qr = p2(q.c, q.s), q0 = p2(1.0f, 0.0f);
+        qA = rA ? qr : q0;
+        qB = rB ? qr : q0;
+    }
+    // an island the ONE_ROT rotations hold for: every contact (this lane's, when `mine`) has at most
+    // one rotating body and its fixed bodies start at angle +0
+    __device__ __forceinline__ static bool one_rot_contact_bad(bool rA, bool rB, float angA, float angB) {
+        return (rA && rB) || (!rA && __float_as_uint(angA) != 0u) || (!rB && __float_as_uint(angB) != 0u);
+    }
+    // the register-resident form: identical lanes, one wave-uniform rotation source
+    template <class Rots>
     __device__ __forceinline__ static void pcc_update(const PCC& c, P2& cA, float& aA, P2& cB, float& aB, float& minSep,
-                                                      float baum, UniMemo& memo) {
-        auto get = [&memo](float a) { return memo.get(a); };
-        pos_update(c, __builtin_amdgcn_readfirstlane(c.pcount), __builtin_amdgcn_readfirstlane(c.type), baum, get, get,
-                   [&minSep](float sep) { minSep = fmin_(minSep, sep); }, cA, aA, cB, aB);
+                                                      float baum, Rots&& rots) {
+        pos_update(c, c.pcount, c.type, baum, rots, [&minSep](float sep) { minSep = fmin_(minSep, sep); }, cA, aA, cB, aB);
     }
     // NC = 1: contact 0 on (P, Q).  NC = 2: SAMEB - both contacts on P, Q (contact 1 as (P, Q) if
     // XA1 else (Q, P)); otherwise X (= P) shared, Y (= Q) the other body of contact 0, Z of contact 1,
@@ -2056,19 +1831,73 @@ template <int ENV> struct World {
         float aP = is.pa[p], aQ = is.pa[q], aZ = is.pa[z];
         const float baum = toi ? TOI_BAUMGARTE : BAUMGARTE;
         const float exitSep = toi ? -1.5f * LINEAR_SLOP : -3.0f * LINEAR_SLOP;
-        UniMemo memo;
-        int it = 0;
-        while (it < iters) {
-            ++it;
+        // one pass; `with(k, upd)` runs contact k's update `upd(rots)` with the rotations it chooses
+        // (the choice is per contact, so each arm is straight-line code); returns the minimum separation
+        auto pass = [&](auto&& with) {
             float minSep = 0.0f;
             if (NC == 1 || SAMEB) {
-                if (XA0) pcc_update(c0, cP, aP, cQ, aQ, minSep, baum, memo); else pcc_update(c0, cQ, aQ, cP, aP, minSep, baum, memo);
-                if (NC == 2) { if (XA1) pcc_update(c1, cP, aP, cQ, aQ, minSep, baum, memo); else pcc_update(c1, cQ, aQ, cP, aP, minSep, baum, memo); }
+                if (XA0) with(0, [&](auto&& r) { pcc_update(c0, cP, aP, cQ, aQ, minSep, baum, r); });
+                else with(0, [&](auto&& r) { pcc_update(c0, cQ, aQ, cP, aP, minSep, baum, r); });
+                if (NC == 2) {
+                    if (XA1) with(1, [&](auto&& r) { pcc_update(c1, cP, aP, cQ, aQ, minSep, baum, r); });
+                    else with(1, [&](auto&& r) { pcc_update(c1, cQ, aQ, cP, aP, minSep, baum, r); });
+                }
             } else {
-                if (XA0) pcc_update(c0, cP, aP, cQ, aQ, minSep, baum, memo); else pcc_update(c0, cQ, aQ, cP, aP, minSep, baum, memo);
-                if (XA1) pcc_update(c1, cP, aP, cZ, aZ, minSep, baum, memo); else pcc_update(c1, cZ, aZ, cP, aP, minSep, baum, memo);
+                if (XA0) with(0, [&](auto&& r) { pcc_update(c0, cP, aP, cQ, aQ, minSep, baum, r); });
+                else with(0, [&](auto&& r) { pcc_update(c0, cQ, aQ, cP, aP, minSep, baum, r); });
+                if (XA1) with(1, [&](auto&& r) { pcc_update(c1, cP, aP, cZ, aZ, minSep, baum, r); });
+                else with(1, [&](auto&& r) { pcc_update(c1, cZ, aZ, cP, aP, minSep, baum, r); });
             }
-            if (uni(minSep >= exitSep)) break;
+            return minSep;
+        };
+        int it = 0;
+        if constexpr (ONE_ROT) {
+            const bool r0A = __builtin_amdgcn_readfirstlane(c0.iA != 0.0f), r0B = __builtin_amdgcn_readfirstlane(c0.iB != 0.0f);
+            const bool r1A = __builtin_amdgcn_readfirstlane(c1.iA != 0.0f), r1B = __builtin_amdgcn_readfirstlane(c1.iB != 0.0f);
+            const float aY1 = (NC == 1 || SAMEB) ? aQ : aZ;   // contact 1's body other than P
+            bool bad = XA0 ? one_rot_contact_bad(r0A, r0B, aP, aQ) : one_rot_contact_bad(r0A, r0B, aQ, aP);
+            if (NC == 2) bad = bad || (XA1 ? one_rot_contact_bad(r1A, r1B, aP, aY1) : one_rot_contact_bad(r1A, r1B, aY1, aP));
+            bool done = false;
+            if (!uni(bad)) {
+                while (it < iters) {
+                    // the pass-start state, for a redo (every lane writes the same values: no barrier)
+                    is.pcx[p] = cP.x; is.pcy[p] = cP.y; is.pa[p] = aP; is.pcx[q] = cQ.x; is.pcy[q] = cQ.y; is.pa[q] = aQ;
+                    if (NC == 2 && !SAMEB) { is.pcx[z] = cZ.x; is.pcy[z] = cZ.y; is.pa[z] = aZ; }   // z == q otherwise
+                    uint32_t mx = 0u;
+                    const float minSep = pass([&](int k, auto&& upd) {
+                        const bool rA = k == 0 ? r0A : r1A, rB = k == 0 ? r0B : r1B, any = rA || rB;
+                        upd([&mx, rA, rB, any](float a, float b, P2& qa, P2& qb) {
+                            if (any) one_rot(rA, rB, rA ? a : b, qa, qb, mx);
+                            else { qa = p2(1.0f, 0.0f); qb = qa; }   // both fixed (+0): no evaluation
+                        });
+                    });
+                    if (uni(mx >= ROT_FAST_END || aP != aP || aQ != aQ || aZ != aZ)) {   // redo through rot()
+                        cP = p2(is.pcx[p], is.pcy[p]); cQ = p2(is.pcx[q], is.pcy[q]); aP = is.pa[p]; aQ = is.pa[q];
+                        if (NC == 2 && !SAMEB) { cZ = p2(is.pcx[z], is.pcy[z]); aZ = is.pa[z]; }
+                        break;
+                    }
+                    ++it;
+                    if (uni(minSep >= exitSep)) { done = true; break; }
+                }
+            }
+            if (!done) {   // b2Rot::Set of both angles through rot() (glibc's every branch), no lookup
+                while (it < iters) {
+                    ++it;
+                    const float minSep = pass([](int, auto&& upd) {
+                        upd([](float a, float b, P2& qa, P2& qb) { qa = rot_cs(a); qb = rot_cs(b); });
+                    });
+                    if (uni(minSep >= exitSep)) break;
+                }
+            }
+        } else {
+            UniMemo memo;
+            while (it < iters) {
+                ++it;
+                const float minSep = pass([&memo](int, auto&& upd) {
+                    upd([&memo](float a, float b, P2& qa, P2& qb) { qa = memo.get(a); qb = memo.get(b); });
+                });
+                if (uni(minSep >= exitSep)) break;
+            }
         }
         if (tid == 0) {
             is.pcx[p] = cP.x; is.pcy[p] = cP.y; is.pa[p] = aP;
@@ -2094,84 +1923,69 @@ template <int ENV> struct World {
         return -1;
     }
 
-    // position passes of the two-body shapes of solver_velocity_xw (same masks): X and Y in registers,
-    // each (X, W) contact's static body at its fixed centre and angle (+0): a static body's position is
-    // unchanged by a finite impulse (c + 0 * P = c, a + 0 * x = a), so it is not written back.  Same
-    // float operations in the same order as solver_position; one wave-uniform rotation memo.
-    template <int NC, int MASK>
-    MRP_XW_FN int pos_xw(Isl& is, const VC* vcs, const PC* pcs, int iters, int x, int y, int start = 0) {
-        constexpr int FY = xw_first_y<MASK, NC>();
-        PCC c[NC];
-        P2 cW[NC];
-        float aW[NC];
-#pragma unroll
-        for (int i = 0; i < NC; ++i) {
-            c[i] = load_pcc(vcs[i], pcs[i], false, -1, -1);
-            c[i].pcount = __builtin_amdgcn_readfirstlane(c[i].pcount);
-            c[i].type = __builtin_amdgcn_readfirstlane(c[i].type);
-            const int b = vcs[i].ibI;
-            cW[i] = p2(is.pcx[b], is.pcy[b]);
-            aW[i] = is.pa[b];
-        }
-        const P2 mX = c[0].mA;
-        const float iX = c[0].iA;
-        const P2 mY = FY >= 0 ? c[FY >= 0 ? FY : 0].mB : pbc(0.0f);
-        const float iY = FY >= 0 ? c[FY >= 0 ? FY : 0].iB : 0.0f;
-        P2 cX = p2(is.pcx[x], is.pcy[x]), cY = p2(0.0f, 0.0f);
-        float aX = is.pa[x], aY = 0.0f;
-        if (FY >= 0) { cY = p2(is.pcx[y], is.pcy[y]); aY = is.pa[y]; }
-        UniMemo memo;
-        auto get = [&memo](float a) { return memo.get(a); };
-        int it = start;   // passes already run by the lanes path (MRP_XW_LATE_POS)
-        while (it < iters) {
-            ++it;
-            float minSep = 0.0f;
-            auto onSep = [&minSep](float sep) { minSep = fmin_(minSep, sep); };
-#pragma unroll
-            for (int i = 0; i < NC; ++i) {
-                if ((MASK >> i) & 1) {
-                    P2 cb = cW[i];
-                    float ab = aW[i];
-                    pos_update_m(c[i], mX, iX, pbc(0.0f), 0.0f, c[i].pcount, c[i].type, BAUMGARTE, get, get, onSep, cX, aX, cb, ab);
-                } else {
-                    pos_update_m(c[i], mX, iX, mY, iY, c[i].pcount, c[i].type, BAUMGARTE, get, get, onSep, cX, aX, cY, aY);
+    // The lanes path's passes (solver_position_lanes, lanes_passes): `contact(with)` runs one pass, and
+    // for contact i calls `with(i, upd)`, which runs the point updates `upd(rots)` with the rotations
+    // it picks for that contact (per contact, so each arm is straight-line code); the island's
+    // positions live lane-distributed in bx / by / ba.  With ONE_ROT the passes run on the ONE_ROT
+    // rotations while they hold (a contact whose bodies are both fixed evaluates none); a pass that
+    // breaks them is restored (its start state is kept in the island's LDS arrays) and it and the rest
+    // run with b2Rot::Set of both angles through rot().  Otherwise the rotation memo.  Returns the
+    // passes run.
+    template <class Contact>
+    __device__ __forceinline__ int lanes_pass_loop(const PCC& my, bool mine, int cia, int cib, Isl& is, int iters,
+                                                   float exitSep, float& bx, float& by, float& ba, Contact&& contact) {
+        int it = 0;
+        if constexpr (ONE_ROT) {
+            const bool rA = my.iA != 0.0f, rB = my.iB != 0.0f;   // this lane's contact
+            const uint64_t rot_any = __builtin_amdgcn_ballot_w64(rA || rB);   // bit i: contact i has a rotating body
+            bool done = false;
+            if (__builtin_amdgcn_ballot_w64(mine && one_rot_contact_bad(rA, rB, is.pa[cia], is.pa[cib])) == 0) {
+                while (it < iters) {
+                    if (tid < is.nb) { is.pcx[tid] = bx; is.pcy[tid] = by; is.pa[tid] = ba; }   // the pass-start state
+                    uint32_t mx = 0u;   // wave-uniform: the evaluated angles are lane i's
+                    const float minSep = contact([&](int i, auto&& upd) {
+                        const bool any = (rot_any >> i) & 1ull;   // wave-uniform, fixed per contact
+                        upd([&mx, rA, rB, i, any](float a, float b, P2& qa, P2& qb) {
+                            if (any) one_rot(rA, rB, rdl(rA ? a : b, i), qa, qb, mx);
+                            else { qa = p2(1.0f, 0.0f); qb = qa; }   // both fixed (+0): no evaluation (an agent on a wall)
+                        });
+                    });
+                    if (mx >= ROT_FAST_END || uni(ba != ba)) {   // redo this pass through rot()
+                        const int bk = tid < is.nb ? tid : 0;
+                        bx = is.pcx[bk]; by = is.pcy[bk]; ba = is.pa[bk];
+                        break;
+                    }
+                    ++it;
+                    if (minSep >= exitSep) { done = true; break; }
                 }
             }
-            if (uni(minSep >= -3.0f * LINEAR_SLOP)) break;
-        }
-        if (tid == 0) {
-            is.pcx[x] = cX.x; is.pcy[x] = cX.y; is.pa[x] = aX;
-            if (FY >= 0) { is.pcx[y] = cY.x; is.pcy[y] = cY.y; is.pa[y] = aY; }
+            if (!done) {   // b2Rot::Set of both angles through rot() (glibc's every branch), no lookup
+                while (it < iters) {
+                    ++it;
+                    const float minSep = contact([](int i, auto&& upd) {
+                        upd([i](float a, float b, P2& qa, P2& qb) { qa = rot_cs(rdl(a, i)); qb = rot_cs(rdl(b, i)); });
+                    });
+                    if (minSep >= exitSep) break;
+                }
+            }
+        } else {
+            RotMemo memo;
+            while (it < iters) {
+                ++it;
+                // every lane evaluates ITS contact's point updates; the rotations are those of lane i's
+                // angles (wave-uniform), and lane i's result is kept
+                const float minSep = contact([&memo](int i, auto&& upd) {
+                    upd([&memo, i](float a, float b, P2& qa, P2& qb) { qa = memo.get(rdl(a, i)); qb = memo.get(rdl(b, i)); });
+                });
+                if (minSep >= exitSep) break;
+            }
         }
         return it;
     }
-    __device__ __forceinline__ int solver_position_xw_from(Isl& is, const VC* vcs, const PC* pcs, int iters, const XwShape q, int start) {
-        switch (q.key) {
-            case 3 * 16 + 4: return pos_xw<3, 4>(is, vcs, pcs, iters, q.x, q.y, start);
-            case 3 * 16 + 6: return pos_xw<3, 6>(is, vcs, pcs, iters, q.x, q.y, start);
-            case 3 * 16 + 7: return pos_xw<3, 7>(is, vcs, pcs, iters, q.x, q.y, start);
-            case 4 * 16 + 12: return pos_xw<4, 12>(is, vcs, pcs, iters, q.x, q.y, start);
-            default: return pos_xw<4, 15>(is, vcs, pcs, iters, q.x, q.y, start);
-        }
-    }
-    __device__ __forceinline__ int solver_position_xw(Isl& is, const VC* vcs, const PC* pcs, int iters) {
-        if constexpr (!XW_PATHS) return -1;
-        const XwShape q = xw_shape(is, vcs);
-        switch (q.key) {
-            case 3 * 16 + 4: return pos_xw<3, 4>(is, vcs, pcs, iters, q.x, q.y);
-            case 3 * 16 + 6: return pos_xw<3, 6>(is, vcs, pcs, iters, q.x, q.y);
-            case 3 * 16 + 7: return pos_xw<3, 7>(is, vcs, pcs, iters, q.x, q.y);
-            case 4 * 16 + 12: return pos_xw<4, 12>(is, vcs, pcs, iters, q.x, q.y);
-            case 4 * 16 + 15: return pos_xw<4, 15>(is, vcs, pcs, iters, q.x, q.y);
-            default: return -1;
-        }
-    }
-
     // position passes of islands of NC = 3 or 4 contacts with the schedule (bodies, point counts,
     // manifold types) read out of the lanes once, before the passes (see lanes_sweeps)
     template <int NC>
-    MRP_LANES_FN int lanes_passes(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB, int iters,
-                                  int stop = 1 << 30, bool* exited = nullptr) {
+    MRP_LANES_FN int lanes_passes(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB, int iters) {
         const int me = tid < NC ? tid : 0;
         const PCC my = load_pcc(vcs[me], pcs[me], toi, toiA, toiB);
         const int cia = vcs[me].iaI, cib = vcs[me].ibI;
@@ -2182,52 +1996,31 @@ template <int ENV> struct World {
         int ia[NC], ib[NC], pc[NC], ty[NC];
 #pragma unroll
         for (int i = 0; i < NC; ++i) { ia[i] = rdli(cia, i); ib[i] = rdli(cib, i); pc[i] = rdli(my.pcount, i); ty[i] = rdli(my.type, i); }
-        RotMemo memo;
-        int it = 0;
-        const int last = stop < iters ? stop : iters;
-        bool ex = false;
-        while (it < last) {
-            ++it;
-            float minSep = 0.0f;
+        const int it = lanes_pass_loop(my, tid < NC, cia, cib, is, iters, exitSep, bx, by, ba, [&](auto&& with) {
+            float minSep = 0.0f;   // wave-uniform: lane i's separations in contact / point order
 #pragma unroll
             for (int i = 0; i < NC; ++i) {
                 P2 cA = p2(rdl(bx, ia[i]), rdl(by, ia[i])); float aA = rdl(ba, ia[i]);
                 P2 cB = p2(rdl(bx, ib[i]), rdl(by, ib[i])); float aB = rdl(ba, ib[i]);
-                auto get = [&memo, i](float a) { return memo.get(rdl(a, i)); };
-                pos_update(my, pc[i], ty[i], baum, get, get, [&minSep, i](float sep) { minSep = fmin_(minSep, rdl(sep, i)); },
-                           cA, aA, cB, aB);
+                with(i, [&](auto&& rots) {
+                    pos_update(my, pc[i], ty[i], baum, rots, [&minSep, i](float sep) { minSep = fmin_(minSep, rdl(sep, i)); },
+                               cA, aA, cB, aB);
+                });
                 bx = wrl(bx, rdl(cA.x, i), ia[i]); by = wrl(by, rdl(cA.y, i), ia[i]); ba = wrl(ba, rdl(aA, i), ia[i]);
                 bx = wrl(bx, rdl(cB.x, i), ib[i]); by = wrl(by, rdl(cB.y, i), ib[i]); ba = wrl(ba, rdl(aB, i), ib[i]);
             }
-            if (minSep >= exitSep) { ex = true; break; }
-        }
+            return minSep;
+        });
         if (tid < is.nb) { is.pcx[tid] = bx; is.pcy[tid] = by; is.pa[tid] = ba; }
-        if (exited) *exited = ex || it >= iters;
         return it;
     }
-    template <int NC>
-    MRP_MAIN_FN int lanes_passes_main(Isl& is, const VC* vcs, const PC* pcs, int iters) {
-#if MRP_XW_LATE_POS
-        if constexpr (XW_LATE_OK) {   // see lanes_sweeps_main
-            const XwShape q = xw_shape(is, vcs);
-            if (xw_supported(q.key)) {
-                bool done = false;
-                const int k = lanes_passes<NC>(is, vcs, pcs, false, -1, -1, iters, MRP_XW_LATE_POS, &done);
-                if (done) return k;
-                return solver_position_xw_from(is, vcs, pcs, iters, q, k);
-            }
-        }
-#endif
-        return lanes_passes<NC>(is, vcs, pcs, false, -1, -1, iters);
-    }
-    template <bool MAIN = false>
     __device__ __forceinline__ int solver_position_lanes(Isl& is, const VC* vcs, const PC* pcs, bool toi, int toiA, int toiB, int iters) {
         // single-block envs only: in the 3-block config the scheduled passes measured slower (-2.7 %,
         // also with 5-8 contact islands scheduled; profiles/r3g_ab_env4_schedules.txt)
         if constexpr (NB == 1) {
             const int n = __builtin_amdgcn_readfirstlane(is.nc);
-            if (n == 3) return MAIN ? lanes_passes_main<3>(is, vcs, pcs, iters) : lanes_passes<3>(is, vcs, pcs, toi, toiA, toiB, iters);
-            if (n == 4) return MAIN ? lanes_passes_main<4>(is, vcs, pcs, iters) : lanes_passes<4>(is, vcs, pcs, toi, toiA, toiB, iters);
+            if (n == 3) return lanes_passes<3>(is, vcs, pcs, toi, toiA, toiB, iters);
+            if (n == 4) return lanes_passes<4>(is, vcs, pcs, toi, toiA, toiB, iters);
         }
         const int nc = is.nc;
         const int me = tid < nc ? tid : 0;   // lanes >= nc evaluate a copy of contact 0 and are never kept
@@ -2238,25 +2031,21 @@ template <int ENV> struct World {
         const float baum = toi ? TOI_BAUMGARTE : BAUMGARTE;
         const float exitSep = toi ? -1.5f * LINEAR_SLOP : -3.0f * LINEAR_SLOP;
         const int ncu = __builtin_amdgcn_readfirstlane(nc);
-        RotMemo memo;
-        int it = 0;
-        while (it < iters) {
-            ++it;
-            float minSep = 0.0f;   // wave-uniform: lane i's separations in contact/point order
+        const int it = lanes_pass_loop(my, tid < nc, cia, cib, is, iters, exitSep, bx, by, ba, [&](auto&& with) {
+            float minSep = 0.0f;   // wave-uniform: lane i's separations in contact / point order
             for (int i = 0; i < ncu; ++i) {
                 const int ia = rdli(cia, i), ib = rdli(cib, i), pcount = rdli(my.pcount, i), type = rdli(my.type, i);
                 P2 cA = p2(rdl(bx, ia), rdl(by, ia)); float aA = rdl(ba, ia);
                 P2 cB = p2(rdl(bx, ib), rdl(by, ib)); float aB = rdl(ba, ib);
-                // every lane evaluates ITS contact's point updates; the rotations are those of lane
-                // i's angles (wave-uniform), and lane i's result is kept
-                auto get = [&memo, i](float a) { return memo.get(rdl(a, i)); };
-                pos_update(my, pcount, type, baum, get, get, [&minSep, i](float sep) { minSep = fmin_(minSep, rdl(sep, i)); },
-                           cA, aA, cB, aB);
+                with(i, [&](auto&& rots) {
+                    pos_update(my, pcount, type, baum, rots, [&minSep, i](float sep) { minSep = fmin_(minSep, rdl(sep, i)); },
+                               cA, aA, cB, aB);
+                });
                 bx = wrl(bx, rdl(cA.x, i), ia); by = wrl(by, rdl(cA.y, i), ia); ba = wrl(ba, rdl(aA, i), ia);
                 bx = wrl(bx, rdl(cB.x, i), ib); by = wrl(by, rdl(cB.y, i), ib); ba = wrl(ba, rdl(aB, i), ib);
             }
-            if (minSep >= exitSep) break;
-        }
+            return minSep;
+        });
         if (tid < is.nb) { is.pcx[tid] = bx; is.pcy[tid] = by; is.pa[tid] = ba; }
         return it;
     }
@@ -2322,8 +2111,7 @@ template <int ENV> struct World {
     __device__ __forceinline__ void island_position(Isl& is, VC* vcs, PC* pcs, int nc) {
         if (nc > 0 && nc <= 64) {
             int n = solver_position_small(is, vcs, pcs, false, -1, -1, 60);
-            if (n < 0) n = solver_position_xw(is, vcs, pcs, 60);
-            if (n < 0) n = solver_position_lanes<true>(is, vcs, pcs, false, -1, -1, 60);
+            if (n < 0) n = solver_position_lanes(is, vcs, pcs, false, -1, -1, 60);
             if (tid == 0) S.posIters += n;
         } else if (tid == 0) {
             if (nc > 0) {
@@ -2351,50 +2139,84 @@ template <int ENV> struct World {
     // at a time by DFS (body list = reverse creation order; contact edges in list order) and runs
     // its serial parts; the wave runs its velocity iterations.  Islands are solved in the
     // reference's order.  The trailing FindNewContacts is issued by world_step_coop.
+    // b2World::Solve's island building, on the whole wave.  The contact list after collide_coop is its
+    // snapshot (sh.clist, list order) less the contacts it destroyed (sh.cover = 0): no contact is
+    // created or destroyed between the two.  Contact k of the list sits in lane k (and k + 64), with its
+    // slot, its bodies and whether it may join an island (enabled and touching), so the reference's
+    // walk of the whole list per popped body - a chain of dependent LDS loads on thread 0 - becomes one
+    // ballot of the candidates, taken in list order (lowest lane first), which is the order the walk
+    // meets them in.  The DFS stack is lane-distributed (entry j in lane j); the body flags, the stack
+    // depth and the counts are wave-uniform.
+    static constexpr int NLW = (C + 63) / 64;   // list words per lane
     __device__ __forceinline__ void solve_coop(float h, float dtRatio) {
         Isl& is = sh.isl;
-        uint32_t bflag = 0;   // body island flags (bit per body), thread 0
-        int seed = ND - 1;    // next DFS seed, thread 0
-        if (tid == 0) for (int c = S.cHead, g_ = 0; c != NULLN && list_ok(g_); c = S.cnext[c]) S.cflags[c] &= ~CF_ISLAND;
+        uint32_t bflag = 0;   // body island flags (bit per body), wave-uniform
+        int seed = ND - 1;    // next DFS seed
+        const int nl = sh.ccount;
+        uint64_t joined[NLW];   // bit k: list contact k joined an island (CF_ISLAND), wave-uniform
+#pragma unroll
+        for (int w = 0; w < NLW; ++w) joined[w] = 0ull;
         for (int nisl = 0;; ++nisl) {
             MRP_PROG(0x3000u + nisl);
             if (nisl > NBODY + 1) { if (tid == 0) S.fault = MRP_FAULT_ISLANDS; break; }
-            if (tid == 0) {
-                while (seed >= 0 && (bflag & (1u << seed))) --seed;
-                sh.isl_go = seed >= 0;
-                if (seed >= 0) {
-                    is.nb = 0; is.nc = 0;
-                    int* stack = sh.stack;
-                    int sc = 0;
-                    stack[sc++] = seed; bflag |= 1u << seed;
-                    for (int g = 0; sc > 0; ++g) {
-                        if (g > 2 * NBODY) { S.fault = MRP_FAULT_DFS; break; }
-                        int b = stack[--sc];
-                        island_add_body(is, b);
-                        if (!is_dyn(b)) continue;
-                        for (int c = S.cHead, g_ = 0; c != NULLN && list_ok(g_); c = S.cnext[c]) {
-                            int bA = L.fix_body[S.cfa[c]], bB = L.fix_body[S.cfb[c]];
-                            if (bA != b && bB != b) continue;
-                            if (S.cflags[c] & CF_ISLAND) continue;
-                            if ((S.cflags[c] & CF_ENABLED) == 0 || (S.cflags[c] & CF_TOUCHING) == 0) continue;
-                            if (is.nc >= C || sc >= NBODY) { S.fault = MRP_FAULT_ISLAND_POOL; continue; }   // never in a valid world
-                            is.contacts[is.nc++] = c;
-                            S.cflags[c] |= CF_ISLAND;
-                            int other = bA == b ? bB : bA;
-                            if (bflag & (1u << other)) continue;
-                            stack[sc++] = other; bflag |= 1u << other;
-                        }
+            while (seed >= 0 && (bflag & (1u << seed))) --seed;
+            if (seed < 0) break;
+            const unsigned long long td = MRP_NOW();
+            int nb = 0, ncs = 0, sc = 0, stk = 0;
+            uint32_t statics = 0u;
+            stk = seed; sc = 1; bflag |= 1u << seed;
+            // this lane's list contacts: slot, bodies, whether they may join an island (read per island,
+            // so nothing of the list stays live in registers across the solver loops)
+            int lslot[NLW], lA[NLW], lB[NLW];
+            bool lok[NLW];
+#pragma unroll
+            for (int w = 0; w < NLW; ++w) {
+                const int k = tid + 64 * w;
+                const bool live = k < nl && sh.cover[k];
+                const int c = live ? sh.clist[k] : 0;
+                lslot[w] = c;
+                lA[w] = live ? (int)L.fix_body[S.cfa[c]] : -1;
+                lB[w] = live ? (int)L.fix_body[S.cfb[c]] : -1;
+                const int f = live ? S.cflags[c] : 0;
+                lok[w] = live && (f & CF_ENABLED) != 0 && (f & CF_TOUCHING) != 0;
+            }
+            for (int g = 0; sc > 0; ++g) {
+                if (g > 2 * NBODY) { if (tid == 0) S.fault = MRP_FAULT_DFS; break; }
+                const int b = __builtin_amdgcn_readlane(stk, sc - 1);
+                --sc;
+                if (tid == 0) { is.index[b] = nb; is.bodies[nb] = b; }   // island_add_body
+                ++nb;
+                if (!is_dyn(b)) { statics |= 1u << b; continue; }
+#pragma unroll
+                for (int w = 0; w < NLW; ++w) {
+                    uint64_t m = __builtin_amdgcn_ballot_w64(lok[w] && (lA[w] == b || lB[w] == b)) & ~joined[w];
+                    for (int q = 0; m != 0ull && q < 64; ++q) {
+                        const int l = (int)__builtin_ctzll(m);
+                        m &= m - 1ull;
+                        if (ncs >= C || sc >= NBODY) { if (tid == 0) S.fault = MRP_FAULT_ISLAND_POOL; continue; }   // never in a valid world
+                        const int c = __builtin_amdgcn_readlane(lslot[w], l);
+                        const int other = __builtin_amdgcn_readlane(lA[w] == b ? lB[w] : lA[w], l);
+                        if (tid == 0) is.contacts[ncs] = c;
+                        ++ncs;
+                        joined[w] |= 1ull << l;
+                        if (bflag & (1u << other)) continue;
+                        stk = mrp_writelane(other, sc, stk);
+                        ++sc;
+                        bflag |= 1u << other;
                     }
-                    const unsigned long long tp = MRP_NOW();
-                    island_pre(is, h, dtRatio, sh.u.sol.vcs, sh.u.sol.pcs);
-                    MRP_SUB(18, tp);
-#ifdef MRP_STAMPS
-                    if ((uint32_t)is.nc > sh.trace[19]) sh.trace[19] = (uint32_t)is.nc;   // largest island's contacts
-#endif
                 }
             }
+            if (tid == 0) {
+                is.nb = nb; is.nc = ncs;
+                MRP_SUB(32, td);
+                const unsigned long long tp = MRP_NOW();
+                island_pre(is, h, dtRatio, sh.u.sol.vcs, sh.u.sol.pcs);
+                MRP_SUB(18, tp);
+#ifdef MRP_STAMPS
+                if ((uint32_t)is.nc > sh.trace[19]) sh.trace[19] = (uint32_t)is.nc;   // largest island's contacts
+#endif
+            }
             __syncthreads();
-            if (!sh.isl_go) break;
             const int nc = __builtin_amdgcn_readfirstlane(is.nc);
             const unsigned long long tv = MRP_NOW();
             // the lanes with the most contact updates set the kernel's duration: let their
@@ -2403,8 +2225,7 @@ template <int ENV> struct World {
             if (nc > 0 && nc <= 64) {
                 set_prio(lvl > step_prio ? lvl : step_prio);
                 int sweeps = nc == 1 ? solver_velocity_one(is, sh.u.sol.vcs, 180) : (nc == 2 ? solver_velocity_two(is, sh.u.sol.vcs, 180) : -1);
-                if (sweeps < 0) sweeps = solver_velocity_xw(is, sh.u.sol.vcs, 180);
-                if (sweeps < 0) sweeps = solver_velocity_lanes<true>(is, sh.u.sol.vcs, 180);
+                if (sweeps < 0) sweeps = solver_velocity_lanes(is, sh.u.sol.vcs, 180);
                 MRP_TRACE(15, sweeps * nc);
                 (void)sweeps;
             }
@@ -2412,7 +2233,7 @@ template <int ENV> struct World {
             MRP_SUB(16, tv);
             __syncthreads();
             MRP_PROG(0x3400u + nisl);
-            if (tid == 0) island_mid(is, h, sh.u.sol.vcs);
+            if (tid == 0) { const unsigned long long tm = MRP_NOW(); island_mid(is, h, sh.u.sol.vcs); MRP_SUB(33, tm); }
             __syncthreads();
             MRP_PROG(0x3800u + nisl);
             const unsigned long long tq = MRP_NOW();
@@ -2422,12 +2243,24 @@ template <int ENV> struct World {
             __syncthreads();
             MRP_PROG(0x3c00u + nisl);
             if (tid == 0) {
+                const unsigned long long tw = MRP_NOW();
                 island_post(is);
-                for (int i = 0; i < is.nb; ++i) if (!is_dyn(is.bodies[i])) bflag &= ~(1u << is.bodies[i]);
-                --seed;
+                MRP_SUB(33, tw);
+            }
+            bflag &= ~statics;   // static bodies may join later islands
+            --seed;
+        }
+        // the contacts that joined an island carry CF_ISLAND, as after the reference's walk (the flag is
+        // cleared for every listed contact at the start of the solve and set on joining)
+#pragma unroll
+        for (int w = 0; w < NLW; ++w) {
+            const int k = tid + 64 * w;
+            if (k < nl && sh.cover[k]) {
+                const int c = sh.clist[k];
+                S.cflags[c] = ((joined[w] >> tid) & 1ull) ? (S.cflags[c] | CF_ISLAND) : (S.cflags[c] & ~CF_ISLAND);
             }
         }
-        if (tid == 0) for (int b = ND - 1; b >= 0; --b) if (bflag & (1u << b)) sync_fixtures(b);
+        sync_fixtures_coop(bflag);
         __syncthreads();
     }
 
@@ -2598,6 +2431,44 @@ template <int ENV> struct World {
         iB = -1; iA = support(pA, mulT_rv(xA.q, vneg(normal)));
         return vdot(vsub(mul_xv(xA, pA.v[iA]), pointB), normal);
     }
+    // A box around one body's core over its sweep (beta in [0, 1]): every vertex sits at
+    // p(beta) + R(angle(beta)) (v - lc), p linear between c0 and c.  A body whose angle is 0 at both ends
+    // (static bodies, the v0 agents) has R = identity, so its vertex offsets bound it directly;
+    // otherwise every vertex lies within max |v - lc| of p(beta).  Rounding moves the box by ulps.
+    __device__ __forceinline__ static void sweep_box(const DProxy& p, const SweepV& s, V2& lo, V2& hi) {
+        const float px0 = fmin_(s.c0x, s.cx), px1 = fmax_(s.c0x, s.cx), py0 = fmin_(s.c0y, s.cy), py1 = fmax_(s.c0y, s.cy);
+        if (s.a0 == 0.0f && s.a == 0.0f) {
+            float xlo = 3.0e38f, xhi = -3.0e38f, ylo = 3.0e38f, yhi = -3.0e38f;
+            for (int k = 0; k < p.count; ++k) {
+                const float rx = p.v[k].x - s.lcx, ry = p.v[k].y - s.lcy;
+                xlo = fmin_(xlo, rx); xhi = fmax_(xhi, rx); ylo = fmin_(ylo, ry); yhi = fmax_(yhi, ry);
+            }
+            lo = v2(px0 + xlo, py0 + ylo); hi = v2(px1 + xhi, py1 + yhi);
+        } else {
+            float r2 = 0.0f;
+            for (int k = 0; k < p.count; ++k) {
+                const float rx = p.v[k].x - s.lcx, ry = p.v[k].y - s.lcy;
+                r2 = fmax_(r2, rx * rx + ry * ry);
+            }
+            const float R = sqrtf(r2);
+            lo = v2(px0 - R, py0 - R); hi = v2(px1 + R, py1 + R);
+        }
+    }
+    // true when b2TimeOfImpact cannot report e_touching for this pair: it does so only at a time t1 whose
+    // core distance (GJK's, >= the true distance up to rounding; or the separation function's, which at
+    // t1 is at least GJK's distance) is within target + tolerance, and the sweep boxes are farther apart
+    // than that plus a margin of 0.05 m (10 linear slops, far above any rounding of these coordinates).
+    // NaN coordinates never skip.
+    __device__ __forceinline__ static bool toi_far(const DProxy& pA, const SweepV& sA, const DProxy& pB, const SweepV& sB) {
+        V2 aLo, aHi, bLo, bHi;
+        sweep_box(pA, sA, aLo, aHi);
+        sweep_box(pB, sB, bLo, bHi);
+        const float gx = fmax_(fmax_(aLo.x - bHi.x, bLo.x - aHi.x), 0.0f);
+        const float gy = fmax_(fmax_(aLo.y - bHi.y, bLo.y - aHi.y), 0.0f);
+        const float target = fmax_(LINEAR_SLOP, pA.radius + pB.radius - 3.0f * LINEAR_SLOP);
+        const float thr = target + 0.25f * LINEAR_SLOP + 0.05f;
+        return gx * gx + gy * gy > thr * thr;
+    }
     // b2TimeOfImpact; state 3 == e_touching
     __device__ __forceinline__ static TOIOut time_of_impact(const DProxy& pA, const DProxy& pB, SweepV sA, SweepV sB) {
         TOIOut out; out.state = 0; out.t = 1.0f;
@@ -2739,6 +2610,41 @@ template <int ENV> struct World {
         }
         sh.tn = tn; sh.np = np;
     }
+    // The first pass's candidate scan on the whole wave.  At the start of b2World::SolveTOI every sweep's
+    // alpha0 is 0 (solve_toi_coop sets them) and no listed contact carries CF_TOI, so toi_scan's sweep
+    // synchronisation (sweep_advance when the two alpha0 differ) never fires and its per-contact work is
+    // independent: lane k takes list contact k, and only the candidate numbering needs the list order
+    // (a prefix count of the candidates' ballot).  Same candidates, same order, same sweeps as toi_scan.
+    __device__ __forceinline__ void toi_scan_first() {
+        if (tid == 0) {   // the list in order (FindNewContacts has put the new contacts at its head)
+            int n = 0;
+            for (int c = S.cHead, g_ = 0; c != NULLN && list_ok(g_); c = S.cnext[c]) sh.clist[n++] = c;
+            sh.ccount = n;
+        }
+        __syncthreads();
+        const int n = sh.ccount;
+        int tn = 0;
+        for (int k0 = 0; k0 < n; k0 += 64) {
+            const int k = k0 + tid;
+            bool cand = false;
+            int c = 0, bA = 0, bB = 0;
+            if (k < n) {
+                c = sh.clist[k];
+                if ((S.cflags[c] & CF_ENABLED) != 0 && S.ctoiCount[c] <= MAX_SUBSTEPS) {
+                    bA = L.fix_body[S.cfa[c]]; bB = L.fix_body[S.cfb[c]];
+                    cand = !is_dyn(bA) || !is_dyn(bB);   // no bullets in these envs
+                }
+            }
+            const uint64_t m = __builtin_amdgcn_ballot_w64(cand);
+            if (cand) {
+                const int idx = tn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                sh.tcand[idx] = c; sh.u.toi.tsA[idx] = sweep(bA, sh.salpha0); sh.u.toi.tsB[idx] = sweep(bB, sh.salpha0);
+                sh.plan[idx] = idx; sh.pslot[idx] = c;
+            }
+            tn += (int)__popcll(m);
+        }
+        if (tid == 0) { sh.tn = tn; sh.np = tn; }
+    }
     // returns true when an event was processed that needs FindNewContacts
     __device__ __forceinline__ void toi_event(float dt) {
         float* salpha0 = sh.salpha0;
@@ -2849,7 +2755,10 @@ template <int ENV> struct World {
             MRP_PROG(0x2000u + pass);
             if (pass > (MAX_SUBSTEPS + 1) * C + 2) { if (tid == 0) S.fault = MRP_FAULT_TOI_PASSES; break; }
             const unsigned long long ts = MRP_NOW();
-            if (tid == 0) toi_scan();
+            const unsigned long long tsc = MRP_NOW();
+            if (pass == 0) toi_scan_first();
+            else if (tid == 0) toi_scan();
+            MRP_SUB(35, tsc);
             __syncthreads();
             const int tn = sh.tn;
             for (int i = tid; i < tn; i += 64) {
@@ -2857,7 +2766,11 @@ template <int ENV> struct World {
                 int fa = S.cfa[c], fb = S.cfb[c];
                 DProxy pA = {L.shape[fa].v, L.shape[fa].count, L.shape[fa].radius};
                 DProxy pB = {L.shape[fb].v, L.shape[fb].count, L.shape[fb].radius};
-                sh.u.toi.tout[i] = time_of_impact(pA, pB, sh.u.toi.tsA[i], sh.u.toi.tsB[i]);
+                const SweepV sA = sh.u.toi.tsA[i], sB = sh.u.toi.tsB[i];
+                TOIOut o;
+                o.state = 4; o.t = 1.0f;   // e_separated: what b2TimeOfImpact returns for such a pair
+                if (!toi_far(pA, sA, pB, sB)) o = time_of_impact(pA, pB, sA, sB);
+                sh.u.toi.tout[i] = o;
             }
             __syncthreads();
             MRP_SUB(20, ts);   // candidate scan + b2TimeOfImpact of every candidate (the slowest thread's)

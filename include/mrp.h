@@ -201,9 +201,10 @@ int mrp_debug_stamps_ext(int device, uint64_t* pmax16, uint64_t* stepmax256, uin
 /* Diagnostic builds only: the last step's per-lane trace, n_lanes x MRP_TRACE_WORDS words (phase
  * cycles 0-10, total, island contacts, TOI events, position iterations, velocity-solver contact
  * units, velocity-sweep / position-pass / island set-up cycles, the TOI split (20-21), the collide
- * split (22-23), then the lane timeline words).  `out` must hold n_lanes * mrp_debug_trace_words()
+ * split (22-23), the lane timeline words (24-31), then the solve's thread-0 bookkeeping (32 island
+ * building, 33 island write-back + integration, 34 fixture synchronisation) and the TOI scan alone (35)).  `out` must hold n_lanes * mrp_debug_trace_words()
  * words; it is left untouched (MRP_E_STATE) when the library has no diagnostic unit. */
-#define MRP_TRACE_WORDS 32
+#define MRP_TRACE_WORDS 40
 int mrp_debug_trace_words(void);
 int mrp_debug_trace(int device, uint32_t* out, int n_lanes);
 /* Diagnostic builds (-DMRP_PROGRESS) only: allocate n_lanes host-mapped words that every lane's

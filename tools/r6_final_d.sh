@@ -1,0 +1,26 @@
+#!/bin/bash
+# Round-6 final evidence, part D (GPU box): the slowest lane-steps alone of the round-5 library, the final
+# one and the final one with the rotation memo in v0 / Heavy-v0 (libmrp_noonerot.so, MRP_ONE_ROT=0 on
+# their units), then those two envs' driver-window lines of the final library with and without ONE_ROT,
+# interleaved.
+set -uo pipefail
+O=gpurun_out/r6fd
+mkdir -p $O
+( for i in $(seq 1 100); do date >> $O/heartbeat; sleep 15; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+export TMPDIR=/tmp
+timeout -k 10 700 python -u tools/chain_bench.py $O/chain.json --envs 0,1,2,4,5 --repeat 3 --rounds 2 \
+  --libs gym_puzzles_amd/var/libmrp_r5.so,gym_puzzles_amd/libmrp.so,gym_puzzles_amd/libmrp_noonerot.so > $O/chain.log 2>&1 \
+  || { echo "chain bench failed"; tail -20 $O/chain.log; exit 1; }
+tail -4 $O/chain.log
+for r in 0 1; do
+  for lib in libmrp libmrp_noonerot; do
+    for e in 0 1; do
+      MRP_LIB=gym_puzzles_amd/$lib.so timeout -k 10 200 python bench.py --env $e --lanes 4096 --steps 20 --warmup 5 --no-cpu-baseline --single-env 0 \
+          --later-window 0 --episode 0 --multi-step 0 > $O/ab_${lib}_env${e}_$r.log 2>&1 || { echo "bench failed"; tail -20 $O/ab_${lib}_env${e}_$r.log; exit 1; }
+      echo "$r $lib env $e $(tail -1 $O/ab_${lib}_env${e}_$r.log | python3 -c 'import json,sys; print(json.loads(sys.stdin.read())["value"])')"
+    done
+  done
+done
+exit 0
