@@ -46,9 +46,9 @@ def test_step_parity_host_inputs(gpu_lib, orc, env_id):
 @pytest.mark.parametrize("env_id", [0, 1])
 def test_step_parity_block_angle_ranges(gpu_lib, orc, env_id):
     """v0 / Heavy-v0 blocks spawned at angles around and far beyond 120 rad (glibc's sinf / cosf switch
-    to the Payne-Hanek reduction there), and at +-0 and tiny angles: the position passes' ONE_ROT
-    rotations (rot_fast, valid below 120 rad) must hand such passes to the memo path, so every lane
-    stays bit-exact against the oracle."""
+    to the Payne-Hanek reduction there), and at +-0 and tiny angles: the device's rot() evaluates the
+    straight-line fast form (valid below 120 rad) on every lane and replaces its result through glibc's
+    other branches on the lanes at 120 rad or more, so every lane stays bit-exact against the oracle."""
     angles = np.r_[np.linspace(118.5, 121.5, 24), np.linspace(-121.5, -118.5, 16),
                    [0.0, -0.0, 1e-5, -1e-5, 2.0 ** -12, 0.78539816, 125.0, -125.0, 250.0, -250.0, 1e3, -1e3,
                     1e4, 3e4, 7.5e4, -7.5e4, 1e5, 4.0e5, 8.0e5, 1.6e6, 1e6, -1e6, 3.3e6, 5.4e6]]

@@ -206,11 +206,13 @@ def test_dual_schedule_keeps_every_body_in_sequential_order():
         assert got == seq
 
 
-def test_one_rot_fixed_angle_stays_positive_zero():
-    """The position passes' ONE_ROT rotations (mrp_world.h one_rot): a body with invI = 0 whose angle
-    is +0 keeps the bit pattern +0 through every point update (a - 0 * x and a + 0 * x, float32), for
-    every finite x, so its rotation is b2Rot::Set(+0) = {+0, 1}; an infinite or NaN x makes it NaN,
-    which the pass check sends back to the memo path."""
+def test_fixed_angle_stays_positive_zero():
+    """The position passes' rotation memo (mrp_world.h RotMemo / UniMemo) answers an angle whose bits
+    are +0 with b2Rot::Set(+0) = {+0, 1} without a lookup: a body with invI = 0 whose angle is +0 keeps
+    the bit pattern +0 through every point update (a - 0 * x and a + 0 * x, float32) for every finite
+    x, so the agents and walls of v0 / Heavy-v0 take that answer at every point; an infinite or NaN x
+    makes it NaN (then rot() of it, as the reference's b2Rot::Set).  The round-6 ONE_ROT form built
+    on the same property (profiles/r6_one_rot.patch) was measured and dropped."""
     rs = np.random.RandomState(3)
     bits = np.r_[rs.randint(0, 2 ** 32, 200000, dtype=np.uint64).astype(np.uint32),
                  np.array([0, 0x80000000, 1, 0x80000001, 0x7f7fffff, 0xff7fffff, 0x00800000, 0x80800000], np.uint32)]
@@ -225,9 +227,9 @@ def test_one_rot_fixed_angle_stays_positive_zero():
 
 
 def test_rot_fast_end_is_glibc_branch_point():
-    """ROT_FAST_END (0x42f00000, the bits of 120.0f): rot() takes rot_fast exactly when
-    abstop12(y) < abstop12(120.0f), i.e. when the |y| bit pattern is below ROT_FAST_END (NaN and
-    infinities above it)."""
+    """0x42f00000, the bits of 120.0f: the device's rot() keeps its straight-line rot_fast result
+    exactly when abstop12(y) < abstop12(120.0f), i.e. when the |y| bit pattern is below 0x42f00000
+    (NaN and infinities above it), and replaces it through glibc's other branches otherwise."""
     assert int(np.float32(120.0).view(np.uint32)) == 0x42F00000
     rs = np.random.RandomState(5)
     b = rs.randint(0, 2 ** 32, 500000, dtype=np.uint64).astype(np.uint32)

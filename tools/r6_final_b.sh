@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 final evidence, part B (GPU box): every other BASELINE config's driver-window line with its CPU
 # baselines (Heavy-v0, v2, the 3-block config, v3), the Heavy-v0 traffic split, the 2-rank line and the
-# RCCL one-rank line; v0's four windows of the round-5 library and the final one.
+# RCCL one-rank line; v0's four windows of the round-5 library and the final one; both libraries' slowest lane-steps alone.
 set -uo pipefail
 O=gpurun_out/r6fb
 mkdir -p $O
@@ -30,4 +30,8 @@ timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 
 grep '"metric"' $O/bench_rccl1.log | cut -c1-200
 timeout -k 10 700 bash tools/windows_ab.sh r6fb/win "gym_puzzles_amd/var/libmrp_r5.so gym_puzzles_amd/libmrp.so" \
   || { echo "windows failed"; exit 1; }
+timeout -k 10 600 python -u tools/chain_bench.py $O/chain.json --envs 0,1,2,4,5 --repeat 3 --rounds 2 \
+  --libs gym_puzzles_amd/var/libmrp_r5.so,gym_puzzles_amd/libmrp.so > $O/chain.log 2>&1 \
+  || { echo "chain bench failed"; tail -20 $O/chain.log; exit 1; }
+tail -2 $O/chain.log
 exit 0

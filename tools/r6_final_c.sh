@@ -9,7 +9,7 @@ mkdir -p $O
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 export TMPDIR=/tmp
-STAMPS=gym_puzzles_amd/var/stamps_final2.so
+STAMPS=gym_puzzles_amd/var/stamps_final3.so
 for e in 0 1 2; do
   L=4096; [ $e = 2 ] && L=1024
   MRP_LIB=$STAMPS timeout -k 10 200 python tools/issue_capture.py $e $L 5 20 $O/cap_env$e.npz > $O/cap_env$e.log 2>&1 || { echo "capture failed"; tail $O/cap_env$e.log; exit 1; }
