@@ -49,17 +49,13 @@ constexpr int NULLN = -1;
 // MRP_VEL_BFREE=1     the block solver's four cases evaluated together and picked by per-lane selects
 //                     (no chain of case tests, no ballot -> branch); MRP_VEL_BFREE_LANES=1 restricts it to
 //                     the lanes path (3+ contacts)
-// MRP_FRESH_REGS=1    values k_step needs late in the step are made where they are used (v0, v3)
-// MRP_ONE_ROT=0       the position passes of a V == 0 unit (v0, Heavy-v0) keep the rotation memo instead
-//                     of the ONE_ROT form (World::ONE_ROT)
+// MRP_FRESH_REGS=1    values k_step needs late in the step are made where they are used, and the thread id
+//                     is made opaque per island and TOI pass (refresh_tid) (v0, v3)
 // Diagnostic builds (never shipped): MRP_STAMPS (+ MRP_STAMPS_TOI) per-phase timing, MRP_PROGRESS
 // hang localisation.  The arms measured and dropped in rounds 3-5 are kept as patches under
 // profiles/ (r6_dropped_arms.patch), not in this header.
 #ifndef MRP_LANES_PAIRS
 #define MRP_LANES_PAIRS 0
-#endif
-#ifndef MRP_ONE_ROT
-#define MRP_ONE_ROT 1
 #endif
 #ifndef MRP_VEL_PICK2
 #define MRP_VEL_PICK2 0
@@ -333,11 +329,20 @@ template <int ENV> struct World {
     const LdsTables<ENV>& L;
     const EnvTables& T;
     const EnvParams& P;
-    const int tid;
+    int tid;             // made opaque per island / TOI pass by refresh_tid (MRP_FRESH_REGS)
     int step_prio = 0;   // issue priority of this lane for the rest of the step (wave-uniform)
     int prio_floor = 0;  // lower bound for step_prio (k_step: from the lane's previous-step cost)
 
     __device__ __forceinline__ World(SH& s, const EnvTables& t, const EnvParams& p, int thread) : sh(s), S(s.S), L(s.lt), T(t), P(p), tid(thread) {}
+
+    // MRP_FRESH_REGS: a copy of tid the compiler cannot prove equal to the one before it, so the LDS
+    // addresses derived from it are made inside the loop that refreshes it, not hoisted to k_step's
+    // entry and kept (or spilled) across the whole step
+    __device__ __forceinline__ void refresh_tid() {
+#if MRP_FRESH_REGS
+        asm volatile("" : "+v"(tid));
+#endif
+    }
 
     // ------------------------------------------------------------------ bodies
     __device__ __forceinline__ bool is_dyn(int b) const { return b < ND; }
@@ -1784,32 +1789,6 @@ template <int ENV> struct World {
             aB += iB * pcross(rB, Pv);
         }
     }
-    // Rotations of a contact with at most one rotating body (invI != 0 after the TOI masking) in an
-    // island whose other bodies' angles are +0 (ONE_ROT islands: every island of v0 / Heavy-v0, whose
-    // agents have density 0, hence invI = 0, and spawn at angle 0, beside static walls).  A fixed
-    // body's angle stays +0 through the passes (a - 0 * x = +0 and a + 0 * x = +0 for every finite x;
-    // an infinite or NaN x makes it NaN), so its rotation is b2Rot::Set(+0) = {+0, 1} with no lookup.
-    // The rotating body's b2Rot::Set is evaluated at every point, straight-line: rot_fast is glibc's
-    // fast-reduction path, which rot() takes for |angle| < 120 rad.  `mx` keeps the largest |angle|
-    // bit pattern evaluated; the caller redoes any pass that met an angle of 120 rad or more, a NaN,
-    // or a fixed angle that went NaN, with b2Rot::Set of both angles through rot() (glibc's every
-    // branch), so every pass has the bits of the reference's (position-pass measurements:
-    // profiles/r6_posbench*.txt).  The other envs' islands (rotating agents) keep the rotation memo.
-    static constexpr bool ONE_ROT = MRP_ONE_ROT && D::V == 0;
-    static constexpr uint32_t ROT_FAST_END = 0x42f00000u;   // |angle| bits of 120.0f (rot(): abstop12 < that of 120)
-    __device__ __forceinline__ static void one_rot(bool rA, bool rB, float r, P2& qA, P2& qB, uint32_t& mx) {
-        const uint32_t m = __float_as_uint(r) & 0x7fffffffu;
-        mx = m > mx ? m : mx;
-        const Rot q = rot_fast(r);
-        const P2 qr = p2(q.c, q.s), q0 = p2(1.0f, 0.0f);
-        qA = rA ? qr : q0;
-        qB = rB ? qr : q0;
-    }
-    // an island the ONE_ROT rotations hold for: every contact (this lane's, when `mine`) has at most
-    // one rotating body and its fixed bodies start at angle +0
-    __device__ __forceinline__ static bool one_rot_contact_bad(bool rA, bool rB, float angA, float angB) {
-        return (rA && rB) || (!rA && __float_as_uint(angA) != 0u) || (!rB && __float_as_uint(angB) != 0u);
-    }
     // the register-resident form: identical lanes, one wave-uniform rotation source
     template <class Rots>
     __device__ __forceinline__ static void pcc_update(const PCC& c, P2& cA, float& aA, P2& cB, float& aB, float& minSep,
@@ -1851,53 +1830,13 @@ template <int ENV> struct World {
             return minSep;
         };
         int it = 0;
-        if constexpr (ONE_ROT) {
-            const bool r0A = __builtin_amdgcn_readfirstlane(c0.iA != 0.0f), r0B = __builtin_amdgcn_readfirstlane(c0.iB != 0.0f);
-            const bool r1A = __builtin_amdgcn_readfirstlane(c1.iA != 0.0f), r1B = __builtin_amdgcn_readfirstlane(c1.iB != 0.0f);
-            const float aY1 = (NC == 1 || SAMEB) ? aQ : aZ;   // contact 1's body other than P
-            bool bad = XA0 ? one_rot_contact_bad(r0A, r0B, aP, aQ) : one_rot_contact_bad(r0A, r0B, aQ, aP);
-            if (NC == 2) bad = bad || (XA1 ? one_rot_contact_bad(r1A, r1B, aP, aY1) : one_rot_contact_bad(r1A, r1B, aY1, aP));
-            bool done = false;
-            if (!uni(bad)) {
-                while (it < iters) {
-                    // the pass-start state, for a redo (every lane writes the same values: no barrier)
-                    is.pcx[p] = cP.x; is.pcy[p] = cP.y; is.pa[p] = aP; is.pcx[q] = cQ.x; is.pcy[q] = cQ.y; is.pa[q] = aQ;
-                    if (NC == 2 && !SAMEB) { is.pcx[z] = cZ.x; is.pcy[z] = cZ.y; is.pa[z] = aZ; }   // z == q otherwise
-                    uint32_t mx = 0u;
-                    const float minSep = pass([&](int k, auto&& upd) {
-                        const bool rA = k == 0 ? r0A : r1A, rB = k == 0 ? r0B : r1B, any = rA || rB;
-                        upd([&mx, rA, rB, any](float a, float b, P2& qa, P2& qb) {
-                            if (any) one_rot(rA, rB, rA ? a : b, qa, qb, mx);
-                            else { qa = p2(1.0f, 0.0f); qb = qa; }   // both fixed (+0): no evaluation
-                        });
-                    });
-                    if (uni(mx >= ROT_FAST_END || aP != aP || aQ != aQ || aZ != aZ)) {   // redo through rot()
-                        cP = p2(is.pcx[p], is.pcy[p]); cQ = p2(is.pcx[q], is.pcy[q]); aP = is.pa[p]; aQ = is.pa[q];
-                        if (NC == 2 && !SAMEB) { cZ = p2(is.pcx[z], is.pcy[z]); aZ = is.pa[z]; }
-                        break;
-                    }
-                    ++it;
-                    if (uni(minSep >= exitSep)) { done = true; break; }
-                }
-            }
-            if (!done) {   // b2Rot::Set of both angles through rot() (glibc's every branch), no lookup
-                while (it < iters) {
-                    ++it;
-                    const float minSep = pass([](int, auto&& upd) {
-                        upd([](float a, float b, P2& qa, P2& qb) { qa = rot_cs(a); qb = rot_cs(b); });
-                    });
-                    if (uni(minSep >= exitSep)) break;
-                }
-            }
-        } else {
-            UniMemo memo;
-            while (it < iters) {
-                ++it;
-                const float minSep = pass([&memo](int, auto&& upd) {
-                    upd([&memo](float a, float b, P2& qa, P2& qb) { qa = memo.get(a); qb = memo.get(b); });
-                });
-                if (uni(minSep >= exitSep)) break;
-            }
+        UniMemo memo;
+        while (it < iters) {
+            ++it;
+            const float minSep = pass([&memo](int, auto&& upd) {
+                upd([&memo](float a, float b, P2& qa, P2& qb) { qa = memo.get(a); qb = memo.get(b); });
+            });
+            if (uni(minSep >= exitSep)) break;
         }
         if (tid == 0) {
             is.pcx[p] = cP.x; is.pcy[p] = cP.y; is.pa[p] = aP;
@@ -1925,60 +1864,20 @@ template <int ENV> struct World {
 
     // The lanes path's passes (solver_position_lanes, lanes_passes): `contact(with)` runs one pass, and
     // for contact i calls `with(i, upd)`, which runs the point updates `upd(rots)` with the rotations
-    // it picks for that contact (per contact, so each arm is straight-line code); the island's
-    // positions live lane-distributed in bx / by / ba.  With ONE_ROT the passes run on the ONE_ROT
-    // rotations while they hold (a contact whose bodies are both fixed evaluates none); a pass that
-    // breaks them is restored (its start state is kept in the island's LDS arrays) and it and the rest
-    // run with b2Rot::Set of both angles through rot().  Otherwise the rotation memo.  Returns the
-    // passes run.
+    // of lane i's angles (wave-uniform) from the rotation memo; the island's positions live
+    // lane-distributed in bx / by / ba.  Returns the passes run.
     template <class Contact>
-    __device__ __forceinline__ int lanes_pass_loop(const PCC& my, bool mine, int cia, int cib, Isl& is, int iters,
-                                                   float exitSep, float& bx, float& by, float& ba, Contact&& contact) {
+    __device__ __forceinline__ int lanes_pass_loop(int iters, float exitSep, Contact&& contact) {
         int it = 0;
-        if constexpr (ONE_ROT) {
-            const bool rA = my.iA != 0.0f, rB = my.iB != 0.0f;   // this lane's contact
-            const uint64_t rot_any = __builtin_amdgcn_ballot_w64(rA || rB);   // bit i: contact i has a rotating body
-            bool done = false;
-            if (__builtin_amdgcn_ballot_w64(mine && one_rot_contact_bad(rA, rB, is.pa[cia], is.pa[cib])) == 0) {
-                while (it < iters) {
-                    if (tid < is.nb) { is.pcx[tid] = bx; is.pcy[tid] = by; is.pa[tid] = ba; }   // the pass-start state
-                    uint32_t mx = 0u;   // wave-uniform: the evaluated angles are lane i's
-                    const float minSep = contact([&](int i, auto&& upd) {
-                        const bool any = (rot_any >> i) & 1ull;   // wave-uniform, fixed per contact
-                        upd([&mx, rA, rB, i, any](float a, float b, P2& qa, P2& qb) {
-                            if (any) one_rot(rA, rB, rdl(rA ? a : b, i), qa, qb, mx);
-                            else { qa = p2(1.0f, 0.0f); qb = qa; }   // both fixed (+0): no evaluation (an agent on a wall)
-                        });
-                    });
-                    if (mx >= ROT_FAST_END || uni(ba != ba)) {   // redo this pass through rot()
-                        const int bk = tid < is.nb ? tid : 0;
-                        bx = is.pcx[bk]; by = is.pcy[bk]; ba = is.pa[bk];
-                        break;
-                    }
-                    ++it;
-                    if (minSep >= exitSep) { done = true; break; }
-                }
-            }
-            if (!done) {   // b2Rot::Set of both angles through rot() (glibc's every branch), no lookup
-                while (it < iters) {
-                    ++it;
-                    const float minSep = contact([](int i, auto&& upd) {
-                        upd([i](float a, float b, P2& qa, P2& qb) { qa = rot_cs(rdl(a, i)); qb = rot_cs(rdl(b, i)); });
-                    });
-                    if (minSep >= exitSep) break;
-                }
-            }
-        } else {
-            RotMemo memo;
-            while (it < iters) {
-                ++it;
-                // every lane evaluates ITS contact's point updates; the rotations are those of lane i's
-                // angles (wave-uniform), and lane i's result is kept
-                const float minSep = contact([&memo](int i, auto&& upd) {
-                    upd([&memo, i](float a, float b, P2& qa, P2& qb) { qa = memo.get(rdl(a, i)); qb = memo.get(rdl(b, i)); });
-                });
-                if (minSep >= exitSep) break;
-            }
+        RotMemo memo;
+        while (it < iters) {
+            ++it;
+            // every lane evaluates ITS contact's point updates; the rotations are those of lane i's
+            // angles (wave-uniform), and lane i's result is kept
+            const float minSep = contact([&memo](int i, auto&& upd) {
+                upd([&memo, i](float a, float b, P2& qa, P2& qb) { qa = memo.get(rdl(a, i)); qb = memo.get(rdl(b, i)); });
+            });
+            if (minSep >= exitSep) break;
         }
         return it;
     }
@@ -1996,7 +1895,7 @@ template <int ENV> struct World {
         int ia[NC], ib[NC], pc[NC], ty[NC];
 #pragma unroll
         for (int i = 0; i < NC; ++i) { ia[i] = rdli(cia, i); ib[i] = rdli(cib, i); pc[i] = rdli(my.pcount, i); ty[i] = rdli(my.type, i); }
-        const int it = lanes_pass_loop(my, tid < NC, cia, cib, is, iters, exitSep, bx, by, ba, [&](auto&& with) {
+        const int it = lanes_pass_loop(iters, exitSep, [&](auto&& with) {
             float minSep = 0.0f;   // wave-uniform: lane i's separations in contact / point order
 #pragma unroll
             for (int i = 0; i < NC; ++i) {
@@ -2031,7 +1930,7 @@ template <int ENV> struct World {
         const float baum = toi ? TOI_BAUMGARTE : BAUMGARTE;
         const float exitSep = toi ? -1.5f * LINEAR_SLOP : -3.0f * LINEAR_SLOP;
         const int ncu = __builtin_amdgcn_readfirstlane(nc);
-        const int it = lanes_pass_loop(my, tid < nc, cia, cib, is, iters, exitSep, bx, by, ba, [&](auto&& with) {
+        const int it = lanes_pass_loop(iters, exitSep, [&](auto&& with) {
             float minSep = 0.0f;   // wave-uniform: lane i's separations in contact / point order
             for (int i = 0; i < ncu; ++i) {
                 const int ia = rdli(cia, i), ib = rdli(cib, i), pcount = rdli(my.pcount, i), type = rdli(my.type, i);
@@ -2158,6 +2057,7 @@ template <int ENV> struct World {
         for (int w = 0; w < NLW; ++w) joined[w] = 0ull;
         for (int nisl = 0;; ++nisl) {
             MRP_PROG(0x3000u + nisl);
+            refresh_tid();
             if (nisl > NBODY + 1) { if (tid == 0) S.fault = MRP_FAULT_ISLANDS; break; }
             while (seed >= 0 && (bflag & (1u << seed))) --seed;
             if (seed < 0) break;
@@ -2753,6 +2653,7 @@ template <int ENV> struct World {
         }
         for (int pass = 0;; ++pass) {
             MRP_PROG(0x2000u + pass);
+            refresh_tid();
             if (pass > (MAX_SUBSTEPS + 1) * C + 2) { if (tid == 0) S.fault = MRP_FAULT_TOI_PASSES; break; }
             const unsigned long long ts = MRP_NOW();
             const unsigned long long tsc = MRP_NOW();
