@@ -196,7 +196,7 @@ def load_valu(env_id: int, lanes: int, first: int, last: int, seed: int, kern_ms
             "source": "oracle op counts of this exact workload (tools/roofline_model.py, profiles/r3_valu_latency.json)"}
 
 
-ISSUE_TABLE = "r5_issue_roofline.json"
+ISSUE_TABLE = "r6_issue_roofline.json"
 
 
 def load_issue(env_id: int, lanes: int, first: int, last: int, seed: int, kern_ms: float):
@@ -208,7 +208,7 @@ def load_issue(env_id: int, lanes: int, first: int, last: int, seed: int, kern_m
     build).  frac = floor / the live kernel_ms.  `lone_wave_ms` is the same lane-step's measured
     duration alone (kernel trace): the model of the launch (the launch lasts as long as its slowest
     lane), whose gap to the floor is latency (dependent chains, LDS and memory waits) and whose gap
-    to kernel_ms is co-resident waves.  None when profiles/r4_issue_roofline.json has no entry."""
+    to kernel_ms is co-resident waves.  None when profiles/ISSUE_TABLE has no entry."""
     path = os.path.join(HERE, "profiles", ISSUE_TABLE)
     try:
         with open(path) as f:
@@ -217,11 +217,14 @@ def load_issue(env_id: int, lanes: int, first: int, last: int, seed: int, kern_m
         return None
     floor_ms = m["issue_floor_us_mean"] * 1e-3
     lone_ms = m["lone_wave_duration_us_mean"] * 1e-3
-    return {"floor_ms": floor_ms, "kernel_ms": kern_ms, "frac": floor_ms / kern_ms,
-            "lone_wave_ms": lone_ms, "lone_wave_over_kernel": lone_ms / kern_ms,
-            "slowest_lane_instructions": m["slowest_lane_instructions_mean"],
-            "in_kernel_clock_ghz": m["in_kernel_clock_ghz"],
-            "source": f"profiles/{ISSUE_TABLE} (tools/issue_capture.py, issue_replay.py, issue_roofline.py)"}
+    out = {"floor_ms": floor_ms, "kernel_ms": kern_ms, "frac": floor_ms / kern_ms,
+           "lone_wave_ms": lone_ms, "lone_wave_over_kernel": lone_ms / kern_ms,
+           "slowest_lane_instructions": m["slowest_lane_instructions_mean"],
+           "in_kernel_clock_ghz": m["in_kernel_clock_ghz"],
+           "source": f"profiles/{ISSUE_TABLE} (tools/issue_capture.py, issue_replay.py, issue_roofline.py)"}
+    if "note" in m:
+        out["note"] = m["note"]
+    return out
 
 
 def load_traffic(env_id: int, lanes: int):
