@@ -61,7 +61,10 @@ _BFREE = ["-DMRP_VEL_BFREE=1", "-DMRP_VEL_PICK2=1", "-DMRP_VEL_VTCROSS=1"]
 # v0 makes the values its step needs late (the state store's per-thread offsets, the TOI phase's
 # zeroes) where they are used (-DMRP_FRESH_REGS=1): VGPR spills 14 -> 4, scratch 48 -> 16 B per
 # thread, PMC traffic 30.9 -> 23.2 MB per launch; driver window -0.4 %, steps 21-220 -0.2 %, whole
-# episode +0.7 % (profiles/r5_windows_traffic_fresh.txt).
+# episode +0.7 % (profiles/r5_windows_traffic_fresh.txt).  Round 6 adds the thread id made opaque per
+# island and TOI pass (refresh_tid): the round-6 code had brought v0 back to 14 spill stores at entry
+# (PMC traffic 37.0 MB per launch); with it 4 (27.6 MB), driver window +0.4 % (profiles/r6_final_ab.txt).
+# On Heavy-v0 / v2 / the 3-block unit it measured +0.4 / -0.5 / -0.9 % (profiles/r6_fresh_more_ab.txt).
 _FRESH = ["-DMRP_FRESH_REGS=1"]
 # v0 takes the branch-free selection (selects form) on its lanes path only (3+ contacts; the one- and
 # two-contact register paths keep the case loop).  Round 6 re-measured it and round 5's two-ballot case
