@@ -76,8 +76,12 @@ _FRESH = ["-DMRP_FRESH_REGS=1"]
 _BFREE_LANES = ["-DMRP_VEL_BFREE=1", "-DMRP_VEL_BFREE_LANES=1"]
 # v3 has the same spill pattern under the iterative-ilp schedule (14 VGPR spills -> 4): PMC traffic
 # 30.8 -> 23.6 MB per launch, slowest lane-steps +0.7 %, driver window level (profiles/r5_ab_v3_fresh.txt).
+# Round 6 (profiles/r6_bfree_paths_ab.txt, three interleaved rounds): the selects form on the lanes path
+# only gives v3 +1.0 % (slowest lane-steps alone and driver window), so v3 takes BFREE_LANES; Heavy-v0
+# +0.4 % with it (within the spread) keeps the case loop; on the register paths only (where v3's TOI
+# sub-step solve runs) v3 measured -1.3 % / -1.5 %.
 UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS + _ITER_ILP + _FRESH + _BFREE_LANES, "mrp_env1.hip": _MAX_ILP, "mrp_env2.hip": _GRANULES + _MAX_ILP + _BFREE,
-              "mrp_env4.hip": _ILP_LOOPS + _BFREE, "mrp_env5.hip": _LANES_PAIRS + _ITER_ILP + _FRESH}
+              "mrp_env4.hip": _ILP_LOOPS + _BFREE, "mrp_env5.hip": _LANES_PAIRS + _ITER_ILP + _FRESH + _BFREE_LANES}
 # -fno-slp-vectorize: the serial solver chains are latency-bound; packing pairs of f32 ops into
 # v_pk_* costs operand-shuffling moves on the dependency chain (measured +2-3 % env-steps/s off)
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
