@@ -80,8 +80,16 @@ _BFREE_LANES = ["-DMRP_VEL_BFREE=1", "-DMRP_VEL_BFREE_LANES=1"]
 # only gives v3 +1.0 % (slowest lane-steps alone and driver window), so v3 takes BFREE_LANES; Heavy-v0
 # +0.4 % with it (within the spread) keeps the case loop; on the register paths only (where v3's TOI
 # sub-step solve runs) v3 measured -1.3 % / -1.5 %.
-UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS + _ITER_ILP + _FRESH + _BFREE_LANES, "mrp_env1.hip": _MAX_ILP, "mrp_env2.hip": _GRANULES + _MAX_ILP + _BFREE,
-              "mrp_env4.hip": _ILP_LOOPS + _BFREE, "mrp_env5.hip": _LANES_PAIRS + _ITER_ILP + _FRESH + _BFREE_LANES}
+# v0 and v3 keep all 4096 lanes of a GPU resident: 4 waves per SIMD (a 128-VGPR budget, 54 VGPR spills).
+# Their driver window is bounded by the slowest lane-step, their steady state by residency: at 4 waves
+# v0's driver window is level (-0.3 / +0.2 %) and steps 21-220 / 501-700 / the whole episode gain
+# +1.1 / +1.4 / +6.1 %; v3 +2.1 / +2.5 / +2.0 % (driver window / 501-700 / whole episode).  At 2 waves
+# v0's steady state lost 7 % (profiles/r6_waves_ab.txt).  Round 3 had chosen 3 waves on the driver window
+# alone (level) and the spills' traffic.
+_W4 = ["-DMRP_STEP_WAVES_PER_EU=4"]
+UNIT_FLAGS = {"mrp_env0.hip": _LANES_PAIRS + _ITER_ILP + _FRESH + _BFREE_LANES + _W4, "mrp_env1.hip": _MAX_ILP,
+              "mrp_env2.hip": _GRANULES + _MAX_ILP + _BFREE, "mrp_env4.hip": _ILP_LOOPS + _BFREE,
+              "mrp_env5.hip": _LANES_PAIRS + _ITER_ILP + _FRESH + _BFREE_LANES + _W4}
 # -fno-slp-vectorize: the serial solver chains are latency-bound; packing pairs of f32 ops into
 # v_pk_* costs operand-shuffling moves on the dependency chain (measured +2-3 % env-steps/s off)
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",

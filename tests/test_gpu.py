@@ -299,11 +299,12 @@ def test_step_device_with_torch_stream(gpu_lib):
     _eq("done", done.cpu().numpy(), h.done)
 
 
-@pytest.mark.parametrize("env_id,lanes,explicit", [(0, 512, True), (1, 4096, False), (5, 4096, False)])
+@pytest.mark.parametrize("env_id,lanes,explicit", [(0, 512, True), (1, 4096, False), (5, 8192, False)])
 def test_costliest_first_schedule_changes_nothing(gpu_lib, env_id, lanes, explicit):
     """Lane scheduling (mrp_set_schedule) only permutes which workgroup steps which lane: every
-    output and the full lane state must be bit-identical to lane-order dispatch.  Envs 1 and 5 at
-    4096 lanes (more than k_step keeps resident) run mrp_create's default, which is costliest-first
+    output and the full lane state must be bit-identical to lane-order dispatch.  Env 1 at 4096
+    lanes and env 5 at 8192 (more than k_step keeps resident; v3 runs 4 waves per SIMD, so its 4096 lanes
+    are all resident) run mrp_create's default, which is costliest-first
     there (mrp_kernels.hip mrp_create), so the default path's ordering kernel over all lanes is covered."""
     from gym_puzzles_amd import Batch
     steps = 60
